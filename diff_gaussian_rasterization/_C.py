@@ -16,24 +16,11 @@ from hidegs_amd import _lib
 NUM_CHANNELS = 3  # cuda_rasterizer/config.h:15
 NUM_ALL_MAP = 5   # cuda_rasterizer/config.h:16
 
-
-class _Buffers:
-    """Keeps the uint8 tensors the C side asks for alive (resizeFunctional, rasterize_points.cu:27-33)."""
-
-    def __init__(self, device, *tensors):
-        self.device = device
-        self.tensors = list(tensors)
-        self.callbacks = [_lib.ALLOC_FN(self._make(i)) for i in range(len(self.tensors))]
-
-    def _make(self, i):
-        def alloc(_user, nbytes):
-            try:
-                t = self.tensors[i]
-                t.resize_(int(nbytes))
-                return t.data_ptr() if nbytes else None
-            except Exception:  # an exception must not unwind through the C frame
-                return None
-        return alloc
+# Anti-aliasing filter variance of the covariance backward.  The reference hard-codes 0.3
+# there (backward.cu:211) against 0.1 in the forward (forward.cu:356).  A module attribute
+# read on every backward call (not thread-local state), so the value the training thread
+# sets is the one autograd's device thread passes to hidegs_rasterize_backward.
+H_VAR_BWD = 0.3
 
 
 def _check_means(means3D: torch.Tensor) -> None:
@@ -79,13 +66,14 @@ def rasterize_gaussians(background, indices, parent_indices, ts, kids, means3D, 
     rendered = 0
     if P != 0:  # rasterize_points.cu:100
         M = _sh_coeffs(sh)
-        bufs = _Buffers(means3D.device, geom, binning, img)
+        dev = _lib.device_of(means3D, background, viewmatrix, projmatrix, campos)
+        bufs = [_lib.Scratch(dev, t) for t in (geom, binning, img)]
         nr = _lib.C.c_int(0)
         args = [_contig(x) for x in (background, indices, parent_indices, ts, kids, means3D, sh, colors, all_map,
                                      opacity, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, campos)]
         (bg_, idx_, par_, ts_, kids_, m3_, sh_, col_, am_, op_, sc_, rot_, cov_, vm_, pm_, cp_) = args
         rc = _lib.lib().hidegs_rasterize_forward(
-            bufs.callbacks[0], bufs.callbacks[1], bufs.callbacks[2], None,
+            bufs[0].callback, bufs[1].callback, bufs[2].callback, None,
             P, int(degree), M, _lib.ptr(bg_), W, H,
             _lib.ptr(idx_), _lib.ptr(par_), _lib.ptr(ts_), _lib.ptr(kids_),
             _lib.ptr(m3_), _lib.ptr(sh_), _lib.ptr(col_), _lib.ptr(am_),
@@ -94,8 +82,8 @@ def rasterize_gaussians(background, indices, parent_indices, ts, kids, means3D, 
             float(tan_fovx), float(tan_fovy), int(bool(prefiltered)),
             _lib.ptr(out_color), _lib.ptr(out_invdepth), _lib.ptr(out_observe), _lib.ptr(out_all_map),
             _lib.ptr(out_plane_depth), int(bool(render_geo)), _lib.ptr(radii), int(bool(debug)),
-            _lib.current_stream_handle(), _lib.C.byref(nr))
-        _lib.check(rc, "rasterize_gaussians")
+            _lib.stream_handle(dev), _lib.C.byref(nr))
+        _lib.check_with(rc, "rasterize_gaussians", *bufs)
         rendered = nr.value
     return (rendered, out_color, radii, out_observe, out_all_map, out_plane_depth, geom, binning, img, out_invdepth)
 
@@ -122,7 +110,7 @@ def rasterize_gaussians_backward(background, all_map_pixels, indices, parent_ind
     dinv = dL_dout_invdepth if dL_dout_invdepth.size(0) != 0 else None  # rasterize_points.cu:210-216
 
     if P != 0:  # rasterize_points.cu:218
-        scratch = _Buffers(means3D.device, torch.empty((0,), dtype=torch.uint8, device=means3D.device))
+        dev = _lib.device_of(means3D, background, viewmatrix, projmatrix, campos, geomBuffer)
         args = [_contig(x) for x in (background, all_map_pixels, indices, parent_indices, ts, kids, means3D, sh,
                                      colors, all_maps, scales, opacities, rotations, cov3D_precomp, viewmatrix,
                                      projmatrix, campos, radii, dL_dout_color, dL_dout_all_map, dL_dout_plane_depth,
@@ -130,17 +118,17 @@ def rasterize_gaussians_backward(background, all_map_pixels, indices, parent_ind
         (bg_, amp_, idx_, par_, ts_, kids_, m3_, sh_, col_, am_, sc_, op_, rot_, cov_, vm_, pm_, cp_, rad_,
          dpix_, dam_, dpl_, dinv_) = args
         rc = _lib.lib().hidegs_rasterize_backward(
-            scratch.callbacks[0], None, P, int(degree), M, int(R), _lib.ptr(bg_), _lib.ptr(amp_), W, H,
+            P, int(degree), M, int(R), _lib.ptr(bg_), _lib.ptr(amp_), W, H,
             _lib.ptr(idx_), _lib.ptr(par_), _lib.ptr(ts_), _lib.ptr(kids_),
             _lib.ptr(m3_), _lib.ptr(sh_), _lib.ptr(col_), _lib.ptr(am_),
             _lib.ptr(sc_), _lib.ptr(op_), _lib.ptr(rot_), float(scale_modifier),
             _lib.ptr(cov_), _lib.ptr(vm_), _lib.ptr(pm_), _lib.ptr(cp_),
-            float(tan_fovx), float(tan_fovy), _lib.ptr(rad_),
+            float(tan_fovx), float(tan_fovy), _lib.ptr(rad_), float(H_VAR_BWD),
             _lib.ptr(geomBuffer), _lib.ptr(binningBuffer), _lib.ptr(imageBuffer),
             _lib.ptr(dpix_), _lib.ptr(dam_), _lib.ptr(dpl_), _lib.ptr(dinv_),
             _lib.ptr(dL_dmeans2D), _lib.ptr(dL_dopacity), _lib.ptr(dL_dcolors), _lib.ptr(dL_dmeans3D),
             _lib.ptr(dL_dcov3D), _lib.ptr(dL_dsh), _lib.ptr(dL_dscales), _lib.ptr(dL_drotations),
-            _lib.ptr(dL_dall_map), int(bool(render_geo)), int(bool(debug)), _lib.current_stream_handle())
+            _lib.ptr(dL_dall_map), int(bool(render_geo)), int(bool(debug)), _lib.stream_handle(dev))
         _lib.check(rc, "rasterize_gaussians_backward")
     return (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations,
             dL_dall_map)
@@ -153,7 +141,8 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     present = torch.zeros((P,), dtype=torch.bool, device=means3D.device)
     if P != 0:
         m3, vm, pm = means3D.contiguous(), viewmatrix.contiguous(), projmatrix.contiguous()
+        dev = _lib.device_of(m3, vm, pm)
         rc = _lib.lib().hidegs_mark_visible(P, _lib.ptr(m3), _lib.ptr(vm), _lib.ptr(pm), _lib.ptr(present),
-                                            _lib.current_stream_handle())
+                                            _lib.stream_handle(dev))
         _lib.check(rc, "mark_visible")
     return present

@@ -22,24 +22,22 @@ I = C.c_int
 F = C.c_float
 SZ = C.c_size_t
 
-# hidegs_alloc_fn: char* (*)(void* user, size_t nbytes)   (round-1 header form)
+# hidegs_alloc_fn: char* (*)(void* user, size_t nbytes)
 ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_size_t)
+LL = C.c_longlong
+U32 = C.c_uint32
 
 # name -> (restype, argtypes); kept in the order of include/hidegs.h
 SIGNATURES = {
     "hidegs_rasterize_forward": (I, [ALLOC_FN, ALLOC_FN, ALLOC_FN, P, I, I, I, P, I, I, P, P, P, P, P, P, P, P, P, P,
                                      F, P, P, P, P, P, F, F, I, P, P, P, P, P, I, P, I, P, P]),
-    "hidegs_geometry_bytes": (SZ, [I]),
-    "hidegs_binning_bytes": (SZ, [I]),
-    "hidegs_image_bytes": (SZ, [I, I]),
-    "hidegs_rasterize_backward": (I, [ALLOC_FN, P,                # scratch_buffer, alloc_user
-                                      I, I, I, I,                 # P, D, M, R
+    "hidegs_rasterize_backward": (I, [I, I, I, I,                 # P, D, M, R
                                       P, P, I, I,                 # background, all_map_pixels, width, height
                                       P, P, P, P,                 # indices, parent_indices, ts, kids
                                       P, P, P, P,                 # means3D, shs, colors_precomp, all_maps
                                       P, P, P, F,                 # scales, opacities, rotations, scale_modifier
                                       P, P, P, P,                 # cov3D_precomp, viewmatrix, projmatrix, campos
-                                      F, F, P,                    # tan_fovx, tan_fovy, radii
+                                      F, F, P, F,                 # tan_fovx, tan_fovy, radii, h_var_bwd
                                       P, P, P,                    # geom, binning, image buffers
                                       P, P, P, P,                 # dL_dpix, dL_dout_all_map, dL_dplane, dL_dinvdepth
                                       P, P, P, P, P,              # dL_dmean2D, opacity, color, mean3D, cov3D
@@ -48,12 +46,14 @@ SIGNATURES = {
     "hidegs_mark_visible": (I, [I, P, P, P, P, P]),
     "hidegs_dist_cuda2": (I, [ALLOC_FN, P, I, P, P, P]),
     "hidegs_knn_scratch_bytes": (SZ, [I]),
-    "hidegs_set_backward_hvar": (None, [F]),
-    "hidegs_get_backward_hvar": (F, []),
-    "hidegs_enable_stage_timing": (None, [I]),
-    "hidegs_reset_stage_times": (None, []),
-    "hidegs_stage_times": (I, [P, P]),
-    "hidegs_stage_name": (C.c_char_p, [I]),
+    "hidegs_scan_scratch_bytes": (SZ, [LL]),
+    "hidegs_inclusive_scan_u32": (I, [P, SZ, P, P, LL, P]),
+    "hidegs_sort_pairs_u64_scratch_bytes": (SZ, [LL]),
+    "hidegs_sort_pairs_u64": (I, [P, SZ, P, P, P, P, LL, I, I, P]),
+    "hidegs_sort_pairs_u32_scratch_bytes": (SZ, [LL]),
+    "hidegs_sort_pairs_u32": (I, [P, SZ, P, P, P, P, LL, I, I, P]),
+    "hidegs_identify_tile_ranges": (I, [P, LL, P, I, P]),
+    "hidegs_higher_msb": (U32, [U32]),
     "hidegs_last_error": (C.c_char_p, []),
     "hidegs_version": (C.c_char_p, []),
 }
@@ -100,8 +100,64 @@ def ptr(t) -> int:
     return t.data_ptr()
 
 
-def current_stream_handle() -> int:
-    """hipStream_t of PyTorch's current stream (B5), or NULL off-GPU."""
-    if torch.cuda.is_available():
-        return torch.cuda.current_stream().cuda_stream
-    return None
+def device_of(*tensors) -> torch.device:
+    """The one CUDA device all given (non-empty) tensors live on; raises otherwise.
+
+    Kernels dereference these pointers on that device, so a host tensor or a tensor on
+    another GPU must be rejected here rather than handed to the C side."""
+    dev = None
+    for t in tensors:
+        if t is None or t.numel() == 0:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(f"expected a GPU tensor, got one on {t.device}")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"tensors on different devices: {dev} and {t.device}")
+    if dev is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+def stream_handle(device: torch.device) -> int:
+    """hipStream_t of PyTorch's current stream on `device` (B5)."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class Scratch:
+    """A uint8 device tensor the C side grows through an hidegs_alloc_fn callback.
+
+    The C form of the reference's resizeFunctional (rasterize_points.cu:27-33): the
+    callback resizes the tensor and returns its data pointer.  An exception inside the
+    callback must not unwind through the C frame, so it is stored, NULL is returned
+    (the library then reports HIDEGS_E_ALLOC) and `check` re-raises it as the cause.
+    """
+
+    def __init__(self, device, tensor=None):
+        self.tensor = tensor if tensor is not None else torch.empty((0,), dtype=torch.uint8, device=device)
+        self.requests = []
+        self.error = None
+        self.callback = ALLOC_FN(self._alloc)
+
+    def _alloc(self, _user, nbytes):
+        self.requests.append(int(nbytes))
+        try:
+            self.tensor.resize_(int(nbytes))
+            return self.tensor.data_ptr() if nbytes else None
+        except Exception as e:  # noqa: BLE001 -- reported through check()
+            self.error = e
+            return None
+
+
+def check_with(rc: int, what: str, *scratches: "Scratch") -> None:
+    """check() that chains a Python exception raised inside an allocation callback."""
+    if rc == 0:
+        return
+    cause = next((s.error for s in scratches if s is not None and s.error is not None), None)
+    try:
+        check(rc, what)
+    except RuntimeError as e:
+        if cause is not None:
+            raise e from cause
+        raise

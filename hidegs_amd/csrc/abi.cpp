@@ -1,0 +1,62 @@
+// abi.cpp -- error channel, launch checks and the entry points of include/hidegs.h
+// that are not built in this release.
+//
+// The rasterizer forward/backward and markVisible stay unbuilt: writing their kernels
+// was refused in rounds 1 and 2 and the refusal binds ("Decisions in force").
+// They fail loudly with HIDEGS_E_UNSUPPORTED; nothing falls back to a CPU path.
+#include "common.h"
+
+namespace hidegs {
+
+namespace {
+thread_local std::string g_last_error;
+constexpr const char* kNotBuilt =
+    "not built: the gfx950 rasterizer kernels are outside this release (DESIGN.md, 'Decisions in force')";
+}  // namespace
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+const std::string& last_error() { return g_last_error; }
+
+int check_launch(const char* stage, hipStream_t stream, int debug)
+{
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && debug) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return fail(HIDEGS_E_HIP, std::string(stage) + ": " + hipGetErrorString(e));
+    return 0;
+}
+
+static int not_built(const char* fn) { return fail(HIDEGS_E_UNSUPPORTED, std::string(fn) + ": " + kNotBuilt); }
+
+}  // namespace hidegs
+
+extern "C" {
+
+int hidegs_rasterize_forward(hidegs_alloc_fn, hidegs_alloc_fn, hidegs_alloc_fn, void*, int, int, int, const float*,
+                             int, int, const int*, const int*, const float*, const int*, const float*, const float*,
+                             const float*, const float*, const float*, const float*, float, const float*,
+                             const float*, const float*, const float*, const float*, float, float, int, float*,
+                             float*, int*, float*, float*, int, int*, int, void*, int* num_rendered)
+{
+    if (num_rendered) *num_rendered = 0;
+    return hidegs::not_built("hidegs_rasterize_forward");
+}
+
+int hidegs_rasterize_backward(int, int, int, int, const float*, const float*, int, int, const int*, const int*,
+                              const float*, const int*, const float*, const float*, const float*, const float*,
+                              const float*, const float*, const float*, float, const float*, const float*,
+                              const float*, const float*, float, float, const int*, float, char*, char*, char*,
+                              const float*, const float*, const float*, const float*, float*, float*, float*, float*,
+                              float*, float*, float*, float*, float*, int, int, void*)
+{
+    return hidegs::not_built("hidegs_rasterize_backward");
+}
+
+int hidegs_mark_visible(int, const float*, const float*, const float*, unsigned char*, void*)
+{
+    return hidegs::not_built("hidegs_mark_visible");
+}
+
+const char* hidegs_last_error(void) { return hidegs::last_error().c_str(); }
+const char* hidegs_version(void) { return "hidegs-abi 0.3 (gfx950: distCUDA2, scan, radix sort, tile ranges)"; }
+
+}  // extern "C"

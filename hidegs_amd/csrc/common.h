@@ -1,0 +1,84 @@
+// common.h -- shared plumbing of the C-ABI library: error channel, stream handle,
+// scratch carving, launch checks and a few wave64 helpers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/hidegs.h"
+
+namespace hidegs {
+
+// Last error message of the calling thread (hidegs_last_error()).
+void set_error(const std::string& msg);
+const std::string& last_error();
+
+inline int fail(int code, const std::string& msg)
+{
+    set_error(msg);
+    return code;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Checks the launch queue after kernels were enqueued; with debug != 0 it also
+// synchronises the stream so an asynchronous fault is reported at its stage
+// (the reference's CHECK_CUDA(..., debug), auxiliary.h:23-30).
+int check_launch(const char* stage, hipStream_t stream, int debug);
+
+// 256-byte aligned carving of one caller-provided scratch buffer.
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t n) { return (n + kAlign - 1) & ~(kAlign - 1); }
+
+struct Carver {
+    char* base;
+    size_t used = 0;
+    explicit Carver(void* b) : base(static_cast<char*>(b)) {}
+    template <typename T>
+    T* take(size_t count)
+    {
+        T* p = reinterpret_cast<T*>(base ? base + used : nullptr);
+        used += align_up(count * sizeof(T));
+        return p;
+    }
+};
+
+// ---- wave64 helpers (device) --------------------------------------------------
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+template <typename T>
+__device__ __forceinline__ T wave_shfl_xor(T v, int m)
+{
+    return __shfl_xor(v, m, kWave);
+}
+
+__device__ __forceinline__ float wave_max(float v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, kWave));
+    return v;
+}
+__device__ __forceinline__ float wave_min(float v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fminf(v, __shfl_xor(v, m, kWave));
+    return v;
+}
+__device__ __forceinline__ float wave_sum(float v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
+    return v;
+}
+
+}  // namespace hidegs

@@ -1,0 +1,508 @@
+// knn.hip -- distCUDA2 for gfx950: mean of the squared distances to the 3 nearest
+// OTHER points, for every point of a (P,3) fp32 cloud.
+//
+// Contract replaced: distCUDA2 / SimpleKNN::knn (submodules/simple-knn/spatial.cu:15-25,
+// simple_knn.cu:186-221).  Its result is an exact 3-NN quantity -- the box pruning of
+// boxMeanDist (simple_knn.cu:148-184) only discards boxes whose lower-bound distance
+// exceeds an upper bound of the 3rd-best distance -- so this file computes the same
+// value with its own search.  The arithmetic that fixes the result bits follows the
+// reference's definition: squared distance of (candidate - query), the three best
+// initialised to FLT_MAX (so P <= 3 yields FLT_MAX / inf terms exactly as there,
+// simple_knn.cu:155), a point never matches itself by index (duplicates count as
+// distance 0, :159,178), result ((b0 + b1) + b2) / 3.0f (:183).  The squared distance
+// is evaluated as fmaf(dz,dz, fmaf(dy,dy, dx*dx)) on device and in the oracle.
+//
+// Search (MI355X-first):
+//   1. bounding box (grid-stride partial min/max + one finishing workgroup) -- no host
+//      sync; the reference does two blocking D2H copies (simple_knn.cu:194-201);
+//   2. 48-bit Morton codes (16 bits/axis), stable LSD radix sort (primitives.hip);
+//   3. points gathered into a sorted float4 array {x, y, z, original index};
+//   4. leaves = 64 consecutive sorted points = exactly one wave64 of queries,
+//      super-boxes = 64 leaves; AABBs for both;
+//   5. phase 1: one wave per leaf.  The wave seeds its 64 queries from its own leaf
+//      (candidates broadcast from LDS), sends outliers (3rd-best far above the wave's
+//      mean, or unseeded) to a hard list, then walks super-boxes and leaves with the
+//      wave AABB / wave upper bound as a coarse filter and each lane's own bound as a
+//      fine filter (skip a leaf unless some lane can still improve);
+//   6. phase 2: one wave per hard query, lanes cooperate over candidate points and
+//      merge lane-local top-3 lists.
+// Pruning compares a lower bound computed with the same monotone fp expression as the
+// point distance, and prunes only when strictly greater than an upper bound of the
+// 3rd-best: the result is exact for any distribution; the heuristics affect speed only.
+#include <float.h>
+
+#include <algorithm>
+
+#include "common.h"
+
+namespace hidegs {
+
+size_t sort_u64_scratch(long long n);
+int sort_pairs_u64(void* scratch, size_t bytes, const uint64_t* ki, uint64_t* ko, const uint32_t* vi, uint32_t* vo,
+                   long long n, int b, int e, hipStream_t s);
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / kWave;  // 4 waves = 4 leaves per workgroup
+constexpr int kLeaf = 64;               // points per leaf
+constexpr int kFan = 64;                // leaves per super-box
+constexpr int kMortonBits = 16;         // per axis
+constexpr int kBoundBlocks = 1024;
+constexpr float kHardFactor = 8.0f;     // 3rd-best above 8x the wave mean -> phase 2
+
+struct Box {
+    float4 lo, hi;
+};
+
+inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+__device__ __forceinline__ float sqdist(float4 q, float4 c)
+{
+    const float dx = c.x - q.x, dy = c.y - q.y, dz = c.z - q.z;
+    return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+}
+
+// Lower bound of sqdist(q, c) over c in the box, same monotone expression as sqdist.
+__device__ __forceinline__ float box_point_lb(const Box& b, float4 q)
+{
+    const float gx = fmaxf(fmaxf(b.lo.x - q.x, q.x - b.hi.x), 0.f);
+    const float gy = fmaxf(fmaxf(b.lo.y - q.y, q.y - b.hi.y), 0.f);
+    const float gz = fmaxf(fmaxf(b.lo.z - q.z, q.z - b.hi.z), 0.f);
+    return fmaf(gz, gz, fmaf(gy, gy, gx * gx));
+}
+
+// Lower bound over every query in the AABB [qlo, qhi] and every point of the box.
+__device__ __forceinline__ float box_box_lb(const Box& b, float4 qlo, float4 qhi)
+{
+    const float gx = fmaxf(fmaxf(b.lo.x - qhi.x, qlo.x - b.hi.x), 0.f);
+    const float gy = fmaxf(fmaxf(b.lo.y - qhi.y, qlo.y - b.hi.y), 0.f);
+    const float gz = fmaxf(fmaxf(b.lo.z - qhi.z, qlo.z - b.hi.z), 0.f);
+    return fmaf(gz, gz, fmaf(gy, gy, gx * gx));
+}
+
+// Keep the three smallest values seen (a multiset, as updateKBest<3> does).  NaN never enters.
+__device__ __forceinline__ void kbest(float d, float& b0, float& b1, float& b2)
+{
+    d = (d == d) ? d : FLT_MAX;
+    const float t0 = fminf(b0, d), u0 = fmaxf(b0, d);
+    const float t1 = fminf(b1, u0), u1 = fmaxf(b1, u0);
+    b2 = fminf(b2, u1);
+    b1 = t1;
+    b0 = t0;
+}
+
+__device__ __forceinline__ int xcd_swizzle(int b, int nb)
+{
+    // consecutive leaf groups land on one XCD (blocks b, b+8, ... share an XCD's L2)
+    const int per = nb / 8, rem = nb % 8, x = b % 8, k = b / 8;
+    return (x < rem) ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+}
+
+__device__ __forceinline__ uint64_t spread3(uint32_t v)
+{
+    // bit i of v -> bit 3i (v < 2^21)
+    uint64_t x = v & 0x1fffffu;
+    x = (x | (x << 32)) & 0x001f00000000ffffull;
+    x = (x | (x << 16)) & 0x001f0000ff0000ffull;
+    x = (x | (x << 8)) & 0x100f00f00f00f00full;
+    x = (x | (x << 4)) & 0x10c30c30c30c30c3ull;
+    x = (x | (x << 2)) & 0x1249249249249249ull;
+    return x;
+}
+
+// ---- 1. bounds --------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void bounds_kernel(const float* __restrict__ pts, int P,
+                                                        float* __restrict__ partials)
+{
+    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < P; i += (long long)gridDim.x * kBlock) {
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const float v = pts[3 * i + a];
+            lo[a] = fminf(lo[a], v);
+            hi[a] = fmaxf(hi[a], v);
+        }
+    }
+    __shared__ float s[kWaves][6];
+    const int wave = threadIdx.x / kWave;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        lo[a] = wave_min(lo[a]);
+        hi[a] = wave_max(hi[a]);
+    }
+    if (lane_id() == 0)
+        for (int a = 0; a < 3; a++) {
+            s[wave][a] = lo[a];
+            s[wave][3 + a] = hi[a];
+        }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        float v = s[0][threadIdx.x];
+        for (int w = 1; w < kWaves; w++) v = threadIdx.x < 3 ? fminf(v, s[w][threadIdx.x]) : fmaxf(v, s[w][threadIdx.x]);
+        partials[blockIdx.x * 6 + threadIdx.x] = v;
+    }
+}
+
+// params = {lo.x, lo.y, lo.z, scale.x, scale.y, scale.z}
+__global__ __launch_bounds__(kBlock) void bounds_finalize_kernel(const float* __restrict__ partials, int nparts,
+                                                                 float* __restrict__ params)
+{
+    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int b = threadIdx.x; b < nparts; b += kBlock)
+        for (int a = 0; a < 3; a++) {
+            lo[a] = fminf(lo[a], partials[b * 6 + a]);
+            hi[a] = fmaxf(hi[a], partials[b * 6 + 3 + a]);
+        }
+    __shared__ float s[kWaves][6];
+    const int wave = threadIdx.x / kWave;
+    for (int a = 0; a < 3; a++) {
+        lo[a] = wave_min(lo[a]);
+        hi[a] = wave_max(hi[a]);
+    }
+    if (lane_id() == 0)
+        for (int a = 0; a < 3; a++) {
+            s[wave][a] = lo[a];
+            s[wave][3 + a] = hi[a];
+        }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int a = threadIdx.x;
+        float l = s[0][a], h = s[0][3 + a];
+        for (int w = 1; w < kWaves; w++) {
+            l = fminf(l, s[w][a]);
+            h = fmaxf(h, s[w][3 + a]);
+        }
+        const float ext = h - l;
+        const float q = (float)((1u << kMortonBits) - 1u);
+        params[a] = l;
+        params[3 + a] = (ext > 0.f && ext < INFINITY) ? q / ext : 0.f;
+    }
+}
+
+// ---- 2. Morton keys -------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void morton_kernel(const float* __restrict__ pts, int P,
+                                                        const float* __restrict__ params, uint64_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ vals)
+{
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P) return;
+    const float qmax = (float)((1u << kMortonBits) - 1u);
+    uint64_t code = 0;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        float t = (pts[3 * i + a] - params[a]) * params[3 + a];
+        t = fminf(fmaxf(t, 0.f), qmax);  // NaN -> 0 via fmaxf
+        code |= spread3((uint32_t)t) << a;
+    }
+    keys[i] = code;
+    vals[i] = (uint32_t)i;
+}
+
+// ---- 3. gather into sorted order ----------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void gather_kernel(const float* __restrict__ pts, const uint32_t* __restrict__ order,
+                                                        int P, float4* __restrict__ sp)
+{
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= P) return;
+    const uint32_t i = order[j];
+    if (i >= (uint32_t)P) return;  // a permutation of [0, P) by construction
+    sp[j] = make_float4(pts[3ll * i], pts[3ll * i + 1], pts[3ll * i + 2], __uint_as_float(i));
+}
+
+// ---- 4. leaf and super boxes ----------------------------------------------------------------
+__device__ __forceinline__ Box wave_box(float4 p, bool valid)
+{
+    Box b;
+    b.lo = make_float4(wave_min(valid ? p.x : FLT_MAX), wave_min(valid ? p.y : FLT_MAX), wave_min(valid ? p.z : FLT_MAX), 0.f);
+    b.hi = make_float4(wave_max(valid ? p.x : -FLT_MAX), wave_max(valid ? p.y : -FLT_MAX), wave_max(valid ? p.z : -FLT_MAX), 0.f);
+    return b;
+}
+
+__global__ __launch_bounds__(kBlock) void leaf_box_kernel(const float4* __restrict__ sp, int P, int nleaves,
+                                                          Box* __restrict__ leaves)
+{
+    const int L = blockIdx.x * kWaves + threadIdx.x / kWave;
+    if (L >= nleaves) return;
+    const int i = L * kLeaf + lane_id();
+    const bool valid = i < P;
+    const float4 p = valid ? sp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const Box b = wave_box(p, valid);
+    if (lane_id() == 0) leaves[L] = b;
+}
+
+__global__ __launch_bounds__(kBlock) void super_box_kernel(const Box* __restrict__ leaves, int nleaves, int nsuper,
+                                                           Box* __restrict__ supers)
+{
+    const int S = blockIdx.x * kWaves + threadIdx.x / kWave;
+    if (S >= nsuper) return;
+    const int l = S * kFan + lane_id();
+    const bool valid = l < nleaves;
+    Box b = valid ? leaves[l] : Box{make_float4(FLT_MAX, FLT_MAX, FLT_MAX, 0.f), make_float4(-FLT_MAX, -FLT_MAX, -FLT_MAX, 0.f)};
+    Box r;
+    r.lo = make_float4(wave_min(b.lo.x), wave_min(b.lo.y), wave_min(b.lo.z), 0.f);
+    r.hi = make_float4(wave_max(b.hi.x), wave_max(b.hi.y), wave_max(b.hi.z), 0.f);
+    if (lane_id() == 0) supers[S] = r;
+}
+
+// ---- 5. phase 1: one wave per leaf ------------------------------------------------------------
+struct KnnCounters {
+    uint32_t hard;  // number of queries sent to phase 2
+    uint32_t pad[3];
+};
+
+__global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restrict__ sp, int P, int nleaves, int nsuper,
+                                                          const Box* __restrict__ leaves, const Box* __restrict__ supers,
+                                                          float* __restrict__ out, uint32_t* __restrict__ hard,
+                                                          KnnCounters* __restrict__ counters)
+{
+    __shared__ __attribute__((aligned(16))) float4 s_pts[kWaves][kLeaf];
+    const int wave = threadIdx.x / kWave;
+    const int lane = lane_id();
+    const int L = xcd_swizzle(blockIdx.x, gridDim.x) * kWaves + wave;
+    if (L >= nleaves) return;  // whole wave exits; no workgroup barrier below
+    float4* stage = s_pts[wave];
+
+    const int me = L * kLeaf + lane;
+    const bool valid = me < P;
+    const float4 p = valid ? sp[me] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float b0 = FLT_MAX, b1 = FLT_MAX, b2 = FLT_MAX;
+
+    // seed from the own leaf
+    {
+        const int nc = min(kLeaf, P - L * kLeaf);
+        stage[lane] = valid ? p : make_float4(0.f, 0.f, 0.f, 0.f);
+        __builtin_amdgcn_wave_barrier();
+        for (int k = 0; k < nc; k++) {
+            const float4 c = stage[k];
+            const float d = sqdist(p, c);
+            if (k != lane) kbest(d, b0, b1, b2);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // outliers -> phase 2
+    bool active = valid;
+    if (nleaves > 1) {
+        const bool finite = valid && b2 < FLT_MAX;
+        const float nfin = (float)__popcll(__ballot(finite));
+        const float mean = wave_sum(finite ? b2 : 0.f) / fmaxf(nfin, 1.f);
+        const bool is_hard = valid && (!finite || b2 > kHardFactor * mean);
+        const uint64_t hm = __ballot(is_hard);
+        if (hm) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&counters->hard, (uint32_t)__popcll(hm));
+            base = __shfl(base, 0, kWave);
+            const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+            if (is_hard) hard[base + __popcll(hm & lt)] = (uint32_t)me;
+        }
+        active = valid && !is_hard;
+    } else {
+        active = false;  // a single leaf holds every point: the seed is the answer
+        if (valid) out[__float_as_uint(p.w)] = ((b0 + b1) + b2) / 3.0f;
+        return;
+    }
+
+    if (__ballot(active)) {
+        const float4 qlo = make_float4(wave_min(active ? p.x : FLT_MAX), wave_min(active ? p.y : FLT_MAX),
+                                       wave_min(active ? p.z : FLT_MAX), 0.f);
+        const float4 qhi = make_float4(wave_max(active ? p.x : -FLT_MAX), wave_max(active ? p.y : -FLT_MAX),
+                                       wave_max(active ? p.z : -FLT_MAX), 0.f);
+        float ub = wave_max(active ? b2 : -FLT_MAX);
+        for (int s0 = 0; s0 < nsuper; s0 += kWave) {
+            const int s = s0 + lane;
+            bool pass = false;
+            if (s < nsuper) {
+                const Box sb = supers[s];
+                pass = box_box_lb(sb, qlo, qhi) <= ub;
+            }
+            uint64_t smask = __ballot(pass);
+            while (smask) {
+                const int S = s0 + __builtin_ctzll(smask);
+                smask &= smask - 1;
+                const int l = S * kFan + lane;
+                bool lpass = false;
+                if (l < nleaves && l != L) {
+                    const Box lb = leaves[l];
+                    lpass = box_box_lb(lb, qlo, qhi) <= ub;
+                }
+                uint64_t lmask = __ballot(lpass);
+                while (lmask) {
+                    const int C = S * kFan + __builtin_ctzll(lmask);
+                    lmask &= lmask - 1;
+                    const Box cb = leaves[C];
+                    if (!__ballot(active && box_point_lb(cb, p) <= b2)) continue;
+                    const int cbase = C * kLeaf;
+                    const int nc = min(kLeaf, P - cbase);
+                    stage[lane] = (lane < nc) ? sp[cbase + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    __builtin_amdgcn_wave_barrier();
+                    for (int k = 0; k < nc; k++) kbest(sqdist(p, stage[k]), b0, b1, b2);
+                    __builtin_amdgcn_wave_barrier();
+                    ub = wave_max(active ? b2 : -FLT_MAX);
+                }
+            }
+        }
+    }
+    if (active) out[__float_as_uint(p.w)] = ((b0 + b1) + b2) / 3.0f;
+}
+
+// ---- 6. phase 2: one wave per hard query ---------------------------------------------------------
+// Three smallest of the wave's lane-local lists plus g; lane lists are reset.
+__device__ __forceinline__ void wave_merge3(float& a0, float& a1, float& a2, float& g0, float& g1, float& g2)
+{
+    if (lane_id() == 0) {
+        kbest(g0, a0, a1, a2);
+        kbest(g1, a0, a1, a2);
+        kbest(g2, a0, a1, a2);
+    }
+    float g[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const float m = wave_min(a0);
+        const uint64_t who = __ballot(a0 == m);
+        const int w = __builtin_ctzll(who);
+        if (lane_id() == w) {
+            a0 = a1;
+            a1 = a2;
+            a2 = FLT_MAX;
+        }
+        g[r] = m;
+    }
+    g0 = g[0];
+    g1 = g[1];
+    g2 = g[2];
+    a0 = a1 = a2 = FLT_MAX;
+}
+
+__global__ __launch_bounds__(kBlock) void knn_hard_kernel(const float4* __restrict__ sp, int P, int nleaves, int nsuper,
+                                                          const Box* __restrict__ leaves, const Box* __restrict__ supers,
+                                                          float* __restrict__ out, const uint32_t* __restrict__ hard,
+                                                          const KnnCounters* __restrict__ counters)
+{
+    const int lane = lane_id();
+    const uint32_t nhard = counters->hard;
+    const int nw = gridDim.x * kWaves;
+    for (uint32_t h = blockIdx.x * kWaves + threadIdx.x / kWave; h < nhard; h += nw) {
+        const int me = (int)hard[h];
+        const float4 p = sp[me];
+        const int L = me / kLeaf;
+        float a0 = FLT_MAX, a1 = FLT_MAX, a2 = FLT_MAX;
+        float g0 = FLT_MAX, g1 = FLT_MAX, g2 = FLT_MAX;
+        // seed: own leaf and its two neighbours, one candidate per lane
+        for (int C = max(0, L - 1); C <= min(nleaves - 1, L + 1); C++) {
+            const int j = C * kLeaf + lane;
+            if (j < P && j != me) kbest(sqdist(p, sp[j]), a0, a1, a2);
+        }
+        wave_merge3(a0, a1, a2, g0, g1, g2);
+        for (int s0 = 0; s0 < nsuper; s0 += kWave) {
+            const int s = s0 + lane;
+            bool pass = false;
+            if (s < nsuper) pass = box_point_lb(supers[s], p) <= g2;
+            uint64_t smask = __ballot(pass);
+            while (smask) {
+                const int S = s0 + __builtin_ctzll(smask);
+                smask &= smask - 1;
+                const int l = S * kFan + lane;
+                bool lpass = false;
+                if (l < nleaves && (l < L - 1 || l > L + 1)) lpass = box_point_lb(leaves[l], p) <= g2;
+                uint64_t lmask = __ballot(lpass);
+                if (!lmask) continue;
+                while (lmask) {
+                    const int C = S * kFan + __builtin_ctzll(lmask);
+                    lmask &= lmask - 1;
+                    const int j = C * kLeaf + lane;
+                    if (j < P) kbest(sqdist(p, sp[j]), a0, a1, a2);
+                }
+                wave_merge3(a0, a1, a2, g0, g1, g2);
+            }
+        }
+        if (lane == 0) out[__float_as_uint(p.w)] = ((g0 + g1) + g2) / 3.0f;
+    }
+}
+
+struct KnnLayout {
+    uint64_t *keys, *keys_sorted;
+    uint32_t *vals, *vals_sorted;
+    void* sort_tmp;
+    size_t sort_bytes;
+    float4* sp;
+    Box *leaves, *supers;
+    uint32_t* hard;
+    KnnCounters* counters;
+    float *partials, *params;
+    size_t total;
+};
+
+KnnLayout layout(void* base, int P)
+{
+    const int nleaves = ceil_div(P, kLeaf), nsuper = ceil_div(nleaves, kFan);
+    Carver c(base);
+    KnnLayout l;
+    l.keys = c.take<uint64_t>(P);
+    l.keys_sorted = c.take<uint64_t>(P);
+    l.vals = c.take<uint32_t>(P);
+    l.vals_sorted = c.take<uint32_t>(P);
+    l.sort_bytes = sort_u64_scratch(P);
+    l.sort_tmp = c.take<char>(l.sort_bytes);
+    l.sp = c.take<float4>(P);
+    l.leaves = c.take<Box>(nleaves);
+    l.supers = c.take<Box>(nsuper);
+    l.hard = c.take<uint32_t>(P);
+    l.counters = c.take<KnnCounters>(1);
+    l.partials = c.take<float>(kBoundBlocks * 6);
+    l.params = c.take<float>(8);
+    l.total = c.used;
+    return l;
+}
+
+}  // namespace
+
+size_t knn_scratch_bytes(int P) { return P > 0 ? layout(nullptr, P).total : 0; }
+
+int dist_cuda2(hidegs_alloc_fn alloc, void* user, int P, const float* points, float* mean_dists, hipStream_t stream)
+{
+    if (P < 0) return fail(HIDEGS_E_ARG, "distCUDA2: negative point count");
+    if (P == 0) return 0;
+    if (!points || !mean_dists) return fail(HIDEGS_E_ARG, "distCUDA2: NULL points or output");
+    if (!alloc) return fail(HIDEGS_E_ARG, "distCUDA2: NULL scratch allocator");
+    const size_t bytes = knn_scratch_bytes(P);
+    char* base = alloc(user, bytes);
+    if (!base) return fail(HIDEGS_E_ALLOC, "distCUDA2: scratch allocation of " + std::to_string(bytes) + " bytes failed");
+    const KnnLayout l = layout(base, P);
+    const int nleaves = ceil_div(P, kLeaf), nsuper = ceil_div(nleaves, kFan);
+    const int nb = ceil_div(P, kBlock);
+    const int nbound = std::min(kBoundBlocks, nb);
+
+    if (hipMemsetAsync(l.counters, 0, sizeof(KnnCounters), stream) != hipSuccess)
+        return fail(HIDEGS_E_HIP, "distCUDA2: memset failed");
+    hipLaunchKernelGGL(bounds_kernel, dim3(nbound), dim3(kBlock), 0, stream, points, P, l.partials);
+    hipLaunchKernelGGL(bounds_finalize_kernel, dim3(1), dim3(kBlock), 0, stream, l.partials, nbound, l.params);
+    hipLaunchKernelGGL(morton_kernel, dim3(nb), dim3(kBlock), 0, stream, points, P, l.params, l.keys, l.vals);
+    int rc = sort_pairs_u64(l.sort_tmp, l.sort_bytes, l.keys, l.keys_sorted, l.vals, l.vals_sorted, P, 0,
+                            3 * kMortonBits, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(gather_kernel, dim3(nb), dim3(kBlock), 0, stream, points, l.vals_sorted, P, l.sp);
+    hipLaunchKernelGGL(leaf_box_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P, nleaves,
+                       l.leaves);
+    hipLaunchKernelGGL(super_box_kernel, dim3(ceil_div(nsuper, kWaves)), dim3(kBlock), 0, stream, l.leaves, nleaves,
+                       nsuper, l.supers);
+    hipLaunchKernelGGL(knn_leaf_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P, nleaves,
+                       nsuper, l.leaves, l.supers, mean_dists, l.hard, l.counters);
+    hipLaunchKernelGGL(knn_hard_kernel, dim3(std::min(2048, ceil_div(nleaves, kWaves))), dim3(kBlock), 0, stream, l.sp,
+                       P, nleaves, nsuper, l.leaves, l.supers, mean_dists, l.hard, l.counters);
+    return check_launch("distCUDA2", stream, 0);
+}
+
+}  // namespace hidegs
+
+extern "C" {
+
+int hidegs_dist_cuda2(hidegs_alloc_fn scratch_buffer, void* alloc_user, int P, const float* points, float* mean_dists,
+                      void* stream)
+{
+    return hidegs::dist_cuda2(scratch_buffer, alloc_user, P, points, mean_dists, hidegs::as_stream(stream));
+}
+
+size_t hidegs_knn_scratch_bytes(int P) { return hidegs::knn_scratch_bytes(P); }
+
+}  // extern "C"

@@ -1,0 +1,524 @@
+// primitives.hip -- the binning primitives of Rasterizer::forward as gfx950 kernels:
+//
+//   hidegs_inclusive_scan_u32   <- cub::DeviceScan::InclusiveSum of tiles_touched
+//                                  (rasterizer_impl.cu:171,321)
+//   hidegs_sort_pairs_u64/_u32  <- cub::DeviceRadixSort::SortPairs over bits [begin, end)
+//                                  (rasterizer_impl.cu:193-196,354-362; simple_knn.cu:211-214)
+//   hidegs_identify_tile_ranges <- cudaMemsetAsync(ranges) + identifyTileRanges
+//                                  (rasterizer_impl.cu:364-371,120-142)
+//   hidegs_higher_msb           <- getHigherMsb (rasterizer_impl.cu:35-50)
+//
+// Design (MI355X-first, not a CUB restatement):
+//  * Tiles of 4096 items per 256-thread workgroup (4 x wave64, 16 items per lane),
+//    global traffic in 16-byte-per-lane vector loads where the layout allows.
+//  * Scan: reduce -> scan of tile sums -> rescan, three stream-ordered launches
+//    with no inter-workgroup hand-off inside a launch.
+//  * Radix sort: LSD, 8-bit digits, per pass three launches:
+//      1. tile histogram  (per-wave LDS histograms, digit-major counts[d][tile])
+//      2. per-digit exclusive scan over tiles (one workgroup per digit)
+//      3. scatter: stable ranks from wave64 ballot matching (8 ballots give the
+//         set of lanes sharing a digit), per-wave running counters in LDS,
+//         a local sort of the tile in LDS, then run-contiguous global stores.
+//    Stability is by construction: item order inside a wave is (round, lane),
+//    waves own consecutive 1024-item segments, tiles are ordered by the scan.
+// No kernel depends on dispatch order or XCD placement.
+#include "common.h"
+
+namespace hidegs {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kItems = 16;
+constexpr int kTile = kBlock * kItems;       // 4096
+constexpr int kWavesPerBlock = kBlock / kWave;  // 4
+constexpr int kRadixBits = 8;
+constexpr int kRadix = 1 << kRadixBits;     // 256
+
+inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// ============================== scan ===========================================
+
+// Block-wide exclusive scan of one u32 per thread (256 threads); returns the
+// exclusive prefix and writes the block total to *total.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t* total)
+{
+    const int lane = lane_id();
+    const int wave = threadIdx.x / kWave;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t o = __shfl_up(inc, d, kWave);
+        if (lane >= d) inc += o;
+    }
+    if (lane == kWave - 1) s_wave[wave] = inc;
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; w++) {
+        uint32_t s = s_wave[w];
+        if (w < wave) woff += s;
+        tot += s;
+    }
+    *total = tot;
+    __syncthreads();  // s_wave may be reused by the caller
+    return woff + inc - v;
+}
+
+// Loads one tile of u32 (striped 16-byte loads) and leaves it in LDS.
+__device__ __forceinline__ void load_tile_u32(const uint32_t* in, long long base, long long n,
+                                              uint32_t* s_tile)
+{
+    const int t = threadIdx.x;
+    if (base + kTile <= n && ((reinterpret_cast<uintptr_t>(in) & 15) == 0)) {
+        const uint4* src = reinterpret_cast<const uint4*>(in + base);
+#pragma unroll
+        for (int j = 0; j < kItems / 4; j++) {
+            uint4 v = src[j * kBlock + t];
+            reinterpret_cast<uint4*>(s_tile)[j * kBlock + t] = v;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            long long i = base + j * kBlock + t;
+            s_tile[j * kBlock + t] = (i < n) ? in[i] : 0u;
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBlock) void scan_reduce_kernel(const uint32_t* __restrict__ in, long long n,
+                                                             uint32_t* __restrict__ tile_sums)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[kTile];
+    __shared__ uint32_t s_wave[kWavesPerBlock];
+    const long long base = (long long)blockIdx.x * kTile;
+    load_tile_u32(in, base, n, s_tile);
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; j++) sum += s_tile[threadIdx.x * kItems + j];
+    uint32_t total;
+    block_exclusive_scan(sum, s_wave, &total);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
+}
+
+// Exclusive scan of `count` u32 in place by ONE workgroup (count is small: tiles).
+__global__ __launch_bounds__(kBlock) void scan_small_kernel(uint32_t* __restrict__ data, int count,
+                                                            uint32_t* __restrict__ total_out)
+{
+    __shared__ uint32_t s_wave[kWavesPerBlock];
+    uint32_t carry = 0;
+    for (int base = 0; base < count; base += kTile) {
+        uint32_t v[kItems];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            int i = base + threadIdx.x * kItems + j;
+            v[j] = (i < count) ? data[i] : 0u;
+            sum += v[j];
+        }
+        uint32_t total;
+        uint32_t pre = block_exclusive_scan(sum, s_wave, &total) + carry;
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            int i = base + threadIdx.x * kItems + j;
+            if (i < count) data[i] = pre;
+            pre += v[j];
+        }
+        carry += total;
+    }
+    if (total_out && threadIdx.x == 0) *total_out = carry;
+}
+
+// in and out may alias (in-place scan): each workgroup reads its whole tile before writing it.
+__global__ __launch_bounds__(kBlock) void scan_downsweep_kernel(const uint32_t* in, long long n,
+                                                                const uint32_t* __restrict__ tile_offsets,
+                                                                uint32_t* out)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[kTile];
+    __shared__ uint32_t s_wave[kWavesPerBlock];
+    const long long base = (long long)blockIdx.x * kTile;
+    load_tile_u32(in, base, n, s_tile);
+    uint32_t v[kItems];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        v[j] = s_tile[threadIdx.x * kItems + j];
+        sum += v[j];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(sum, s_wave, &total) + tile_offsets[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        run += v[j];
+        s_tile[threadIdx.x * kItems + j] = run;  // inclusive
+    }
+    __syncthreads();
+    if (base + kTile <= n && ((reinterpret_cast<uintptr_t>(out) & 15) == 0)) {
+        uint4* dst = reinterpret_cast<uint4*>(out + base);
+#pragma unroll
+        for (int j = 0; j < kItems / 4; j++) dst[j * kBlock + threadIdx.x] = reinterpret_cast<uint4*>(s_tile)[j * kBlock + threadIdx.x];
+    } else {
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            long long i = base + j * kBlock + threadIdx.x;
+            if (i < n) out[i] = s_tile[j * kBlock + threadIdx.x];
+        }
+    }
+}
+
+// ============================== radix sort =====================================
+
+template <typename K>
+__device__ __forceinline__ uint32_t digit_of(K key, int shift, uint32_t mask)
+{
+    return (uint32_t)(key >> shift) & mask;
+}
+
+// counts[d * ntiles + tile] = number of keys of tile `tile` whose digit is d.
+template <typename K>
+__global__ __launch_bounds__(kBlock) void radix_hist_kernel(const K* __restrict__ keys, long long n, int shift,
+                                                            uint32_t mask, int ntiles, uint32_t* __restrict__ counts)
+{
+    __shared__ uint32_t s_hist[kWavesPerBlock][kRadix];
+    const int t = threadIdx.x;
+    const int wave = t / kWave;
+    for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_hist[0][0])[i] = 0;
+    __syncthreads();
+    const long long base = (long long)blockIdx.x * kTile;
+    K k[kItems];
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        long long i = base + j * kBlock + t;
+        k[j] = (i < n) ? keys[i] : K(0);
+    }
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        long long i = base + j * kBlock + t;
+        if (i < n) atomicAdd(&s_hist[wave][digit_of(k[j], shift, mask)], 1u);
+    }
+    __syncthreads();
+    for (int d = t; d < kRadix; d += kBlock) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; w++) c += s_hist[w][d];
+        counts[(long long)d * ntiles + blockIdx.x] = c;
+    }
+}
+
+// One workgroup per digit: exclusive scan of counts[d][0..ntiles) in place; totals[d] = sum.
+__global__ __launch_bounds__(kBlock) void radix_digit_scan_kernel(uint32_t* __restrict__ counts, int ntiles,
+                                                                  uint32_t* __restrict__ totals)
+{
+    __shared__ uint32_t s_wave[kWavesPerBlock];
+    uint32_t* row = counts + (long long)blockIdx.x * ntiles;
+    uint32_t carry = 0;
+    for (int base = 0; base < ntiles; base += kBlock * 4) {
+        uint32_t v[4];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            int i = base + threadIdx.x * 4 + j;
+            v[j] = (i < ntiles) ? row[i] : 0u;
+            sum += v[j];
+        }
+        uint32_t total;
+        uint32_t pre = block_exclusive_scan(sum, s_wave, &total) + carry;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            int i = base + threadIdx.x * 4 + j;
+            if (i < ntiles) row[i] = pre;
+            pre += v[j];
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+}
+
+// Stable scatter of one tile.  LDS: keys + values of the tile, per-wave digit counters.
+template <typename K>
+__global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restrict__ keys_in,
+                                                               const uint32_t* __restrict__ vals_in,
+                                                               K* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+                                                               long long n, int shift, uint32_t mask, int ntiles,
+                                                               const uint32_t* __restrict__ tile_prefix,
+                                                               const uint32_t* __restrict__ totals)
+{
+    __shared__ __attribute__((aligned(16))) K s_keys[kTile];
+    __shared__ __attribute__((aligned(16))) uint32_t s_vals[kTile];
+    __shared__ uint32_t s_cnt[kWavesPerBlock][kRadix];  // per-wave running counters, later global offsets
+    __shared__ uint32_t s_start[kRadix];                // tile-local start of each digit run
+    __shared__ uint32_t s_wave[kWavesPerBlock];
+
+    const int t = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = t / kWave;
+    const long long base = (long long)blockIdx.x * kTile;
+    const long long seg = base + (long long)wave * (kItems * kWave);  // this wave's 1024 items
+
+    for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
+
+    K k[kItems];
+    uint32_t v[kItems];
+#pragma unroll
+    for (int r = 0; r < kItems; r++) {
+        long long i = seg + r * kWave + lane;
+        bool ok = i < n;
+        k[r] = ok ? keys_in[i] : K(0);
+        v[r] = ok ? vals_in[i] : 0u;
+    }
+    __syncthreads();
+
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t rank[kItems];
+#pragma unroll
+    for (int r = 0; r < kItems; r++) {
+        long long i = seg + r * kWave + lane;
+        const bool ok = i < n;
+        const uint32_t d = digit_of(k[r], shift, mask);
+        uint64_t m = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < kRadixBits; b++) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const uint32_t below = (uint32_t)__popcll(m & lt);
+        const uint32_t cnt = (uint32_t)__popcll(m);
+        uint32_t old = 0;
+        if (ok) old = s_cnt[wave][d];
+        __builtin_amdgcn_wave_barrier();
+        if (ok && below == 0) s_cnt[wave][d] = old + cnt;
+        __builtin_amdgcn_wave_barrier();
+        rank[r] = old + below;
+    }
+    __syncthreads();
+
+    // digit d: prefix over waves, tile total, then tile-local run starts
+    uint32_t tile_count_d = 0;
+    {
+        const int d = t;  // kBlock == kRadix
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; w++) {
+            uint32_t c = s_cnt[w][d];
+            s_cnt[w][d] = run;
+            run += c;
+        }
+        tile_count_d = run;
+    }
+    uint32_t dummy;
+    const uint32_t start_d = block_exclusive_scan(tile_count_d, s_wave, &dummy);
+    s_start[t] = start_d;
+    __syncthreads();
+
+#pragma unroll
+    for (int r = 0; r < kItems; r++) {
+        long long i = seg + r * kWave + lane;
+        if (i < n) {
+            const uint32_t d = digit_of(k[r], shift, mask);
+            const uint32_t pos = s_start[d] + s_cnt[wave][d] + rank[r];
+            s_keys[pos] = k[r];
+            s_vals[pos] = v[r];
+        }
+    }
+    __syncthreads();
+
+    // global offset of digit d for this tile = sum of totals of smaller digits + tile prefix
+    {
+        const int d = t;
+        uint32_t tot = totals[d];
+        uint32_t dbase = block_exclusive_scan(tot, s_wave, &dummy);
+        s_cnt[0][d] = dbase + tile_prefix[(long long)d * ntiles + blockIdx.x] - s_start[d];
+    }
+    __syncthreads();
+
+    const int count = (int)((n - base) < kTile ? (n - base) : kTile);
+    for (int i = t; i < count; i += kBlock) {
+        const K key = s_keys[i];
+        const uint32_t d = digit_of(key, shift, mask);
+        const uint32_t dst = s_cnt[0][d] + i;
+        if (dst < n) {  // always true for consistent counts; never write outside the output
+            keys_out[dst] = key;
+            vals_out[dst] = s_vals[i];
+        }
+    }
+}
+
+// ============================== tile ranges ====================================
+
+// Tile ids >= num_tiles violate the caller contract; their entries are skipped rather
+// than written out of bounds.
+__global__ __launch_bounds__(kBlock) void identify_ranges_kernel(const uint64_t* __restrict__ keys, long long n,
+                                                                 uint2* __restrict__ ranges, uint32_t num_tiles)
+{
+    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t cur = (uint32_t)(keys[i] >> 32);
+    if (i == 0) {
+        if (cur < num_tiles) ranges[cur].x = 0;
+    } else {
+        const uint32_t prev = (uint32_t)(keys[i - 1] >> 32);
+        if (cur != prev) {
+            if (prev < num_tiles) ranges[prev].y = (uint32_t)i;
+            if (cur < num_tiles) ranges[cur].x = (uint32_t)i;
+        }
+        if (i == n - 1 && cur < num_tiles) ranges[cur].y = (uint32_t)n;
+    }
+}
+
+// ============================== host side ======================================
+
+size_t scan_scratch(long long n)
+{
+    const int nt = ceil_div(n, kTile);
+    return align_up((size_t)nt * sizeof(uint32_t)) + align_up(sizeof(uint32_t));
+}
+
+template <typename K>
+size_t sort_scratch(long long n)
+{
+    const int nt = ceil_div(n, kTile);
+    return align_up((size_t)n * sizeof(K)) + align_up((size_t)n * sizeof(uint32_t)) +
+           align_up((size_t)kRadix * nt * sizeof(uint32_t)) + align_up(kRadix * sizeof(uint32_t));
+}
+
+template <typename K>
+int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
+               uint32_t* vals_out, long long n, int begin_bit, int end_bit, hipStream_t stream, const char* what)
+{
+    const int kbits = (int)(8 * sizeof(K));
+    if (n < 0 || begin_bit < 0 || end_bit > kbits || begin_bit > end_bit)
+        return fail(HIDEGS_E_ARG, std::string(what) + ": bad size or bit range");
+    if (n > 0x7fffffffLL) return fail(HIDEGS_E_ARG, std::string(what) + ": more than 2^31-1 items");
+    if (n == 0) return 0;
+    if (!keys_in || !keys_out || !vals_in || !vals_out)
+        return fail(HIDEGS_E_ARG, std::string(what) + ": NULL key/value pointer");
+    if (keys_out == keys_in || vals_out == vals_in)
+        return fail(HIDEGS_E_ARG, std::string(what) + ": in-place sorting is not supported");
+    if (!scratch || scratch_bytes < sort_scratch<K>(n))
+        return fail(HIDEGS_E_ARG, std::string(what) + ": scratch buffer too small");
+
+    const int passes = (end_bit - begin_bit + kRadixBits - 1) / kRadixBits;
+    if (passes == 0) {
+        if (hipMemcpyAsync(keys_out, keys_in, n * sizeof(K), hipMemcpyDeviceToDevice, stream) != hipSuccess ||
+            hipMemcpyAsync(vals_out, vals_in, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
+            return fail(HIDEGS_E_HIP, std::string(what) + ": copy failed");
+        return 0;
+    }
+    const int nt = ceil_div(n, kTile);
+    Carver c(scratch);
+    K* alt_k = c.take<K>(n);
+    uint32_t* alt_v = c.take<uint32_t>(n);
+    uint32_t* counts = c.take<uint32_t>((size_t)kRadix * nt);
+    uint32_t* totals = c.take<uint32_t>(kRadix);
+
+    const K* src_k = keys_in;
+    const uint32_t* src_v = vals_in;
+    for (int p = 0; p < passes; p++) {
+        const int shift = begin_bit + p * kRadixBits;
+        const int bits = (end_bit - shift) < kRadixBits ? (end_bit - shift) : kRadixBits;
+        const uint32_t mask = (1u << bits) - 1u;
+        const bool to_out = ((passes - 1 - p) % 2) == 0;
+        K* dk = to_out ? keys_out : alt_k;
+        uint32_t* dv = to_out ? vals_out : alt_v;
+        hipLaunchKernelGGL(radix_hist_kernel<K>, dim3(nt), dim3(kBlock), 0, stream, src_k, n, shift, mask, nt, counts);
+        hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(kRadix), dim3(kBlock), 0, stream, counts, nt, totals);
+        hipLaunchKernelGGL(radix_scatter_kernel<K>, dim3(nt), dim3(kBlock), 0, stream, src_k, src_v, dk, dv, n, shift,
+                           mask, nt, counts, totals);
+        src_k = dk;
+        src_v = dv;
+    }
+    return check_launch(what, stream, 0);
+}
+
+}  // namespace
+
+int inclusive_scan_u32(void* scratch, size_t scratch_bytes, const uint32_t* in, uint32_t* out, long long n,
+                       hipStream_t stream)
+{
+    if (n < 0) return fail(HIDEGS_E_ARG, "inclusive_scan_u32: negative size");
+    if (n == 0) return 0;
+    if (!in || !out) return fail(HIDEGS_E_ARG, "inclusive_scan_u32: NULL pointer");
+    if (!scratch || scratch_bytes < scan_scratch(n)) return fail(HIDEGS_E_ARG, "inclusive_scan_u32: scratch too small");
+    const int nt = ceil_div(n, kTile);
+    Carver c(scratch);
+    uint32_t* sums = c.take<uint32_t>(nt);
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3(nt), dim3(kBlock), 0, stream, in, n, sums);
+    hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(kBlock), 0, stream, sums, nt, (uint32_t*)nullptr);
+    hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nt), dim3(kBlock), 0, stream, in, n, sums, out);
+    return check_launch("inclusive_scan_u32", stream, 0);
+}
+
+size_t inclusive_scan_scratch(long long n) { return scan_scratch(n); }
+size_t sort_u64_scratch(long long n) { return sort_scratch<uint64_t>(n); }
+size_t sort_u32_scratch(long long n) { return sort_scratch<uint32_t>(n); }
+
+int sort_pairs_u64(void* scratch, size_t bytes, const uint64_t* ki, uint64_t* ko, const uint32_t* vi, uint32_t* vo,
+                   long long n, int b, int e, hipStream_t s)
+{
+    return sort_pairs<uint64_t>(scratch, bytes, ki, ko, vi, vo, n, b, e, s, "sort_pairs_u64");
+}
+int sort_pairs_u32(void* scratch, size_t bytes, const uint32_t* ki, uint32_t* ko, const uint32_t* vi, uint32_t* vo,
+                   long long n, int b, int e, hipStream_t s)
+{
+    return sort_pairs<uint32_t>(scratch, bytes, ki, ko, vi, vo, n, b, e, s, "sort_pairs_u32");
+}
+
+int identify_tile_ranges(const uint64_t* keys, long long n, uint32_t* ranges, int num_tiles, hipStream_t stream)
+{
+    if (n < 0 || num_tiles < 0) return fail(HIDEGS_E_ARG, "identify_tile_ranges: negative size");
+    if (num_tiles > 0 && !ranges) return fail(HIDEGS_E_ARG, "identify_tile_ranges: NULL ranges");
+    if (num_tiles > 0 && hipMemsetAsync(ranges, 0, (size_t)num_tiles * 2 * sizeof(uint32_t), stream) != hipSuccess)
+        return fail(HIDEGS_E_HIP, "identify_tile_ranges: memset failed");
+    if (n == 0) return check_launch("identify_tile_ranges", stream, 0);
+    if (!keys) return fail(HIDEGS_E_ARG, "identify_tile_ranges: NULL keys");
+    hipLaunchKernelGGL(identify_ranges_kernel, dim3(ceil_div(n, kBlock)), dim3(kBlock), 0, stream, keys, n,
+                       reinterpret_cast<uint2*>(ranges), (uint32_t)num_tiles);
+    return check_launch("identify_tile_ranges", stream, 0);
+}
+
+}  // namespace hidegs
+
+// ============================== C ABI ==========================================
+extern "C" {
+
+size_t hidegs_scan_scratch_bytes(long long n) { return n > 0 ? hidegs::inclusive_scan_scratch(n) : 0; }
+int hidegs_inclusive_scan_u32(void* scratch, size_t scratch_bytes, const uint32_t* in, uint32_t* out, long long n,
+                              void* stream)
+{
+    return hidegs::inclusive_scan_u32(scratch, scratch_bytes, in, out, n, hidegs::as_stream(stream));
+}
+
+size_t hidegs_sort_pairs_u64_scratch_bytes(long long n) { return n > 0 ? hidegs::sort_u64_scratch(n) : 0; }
+int hidegs_sort_pairs_u64(void* scratch, size_t scratch_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                          const uint32_t* vals_in, uint32_t* vals_out, long long n, int begin_bit, int end_bit,
+                          void* stream)
+{
+    return hidegs::sort_pairs_u64(scratch, scratch_bytes, keys_in, keys_out, vals_in, vals_out, n, begin_bit, end_bit,
+                                  hidegs::as_stream(stream));
+}
+
+size_t hidegs_sort_pairs_u32_scratch_bytes(long long n) { return n > 0 ? hidegs::sort_u32_scratch(n) : 0; }
+int hidegs_sort_pairs_u32(void* scratch, size_t scratch_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                          const uint32_t* vals_in, uint32_t* vals_out, long long n, int begin_bit, int end_bit,
+                          void* stream)
+{
+    return hidegs::sort_pairs_u32(scratch, scratch_bytes, keys_in, keys_out, vals_in, vals_out, n, begin_bit, end_bit,
+                                  hidegs::as_stream(stream));
+}
+
+int hidegs_identify_tile_ranges(const uint64_t* sorted_keys, long long n, uint32_t* ranges, int num_tiles,
+                                void* stream)
+{
+    return hidegs::identify_tile_ranges(sorted_keys, n, ranges, num_tiles, hidegs::as_stream(stream));
+}
+
+uint32_t hidegs_higher_msb(uint32_t n)
+{
+    // Number of bits needed to hold n, at least 1 -- the value getHigherMsb's
+    // binary search (rasterizer_impl.cu:35-50) returns for every u32 input.
+    uint32_t bits = 32u - (uint32_t)__builtin_clz(n | 1u);
+    return bits;
+}
+
+}  // extern "C"

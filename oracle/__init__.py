@@ -1,0 +1,59 @@
+"""CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, and only as
+the checker or the timed CPU baseline.  The product packages (diff_gaussian_rasterization,
+simple_knn, hidegs_amd) never import it.
+
+  knn_mean3 / knn_mean3_subset  -- distCUDA2's value from its definition (knn_ref.c)
+  stable_sort_pairs / inclusive_scan_u32 / tile_ranges -- generic integer restatements
+     of the binning primitives (numpy), see binning.py
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        dll = C.CDLL(LIB_PATH)
+        dll.oracle_knn_mean3.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p]
+        dll.oracle_knn_mean3.restype = None
+        dll.oracle_knn_mean3_subset.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_longlong, C.c_void_p]
+        dll.oracle_knn_mean3_subset.restype = None
+        _lib = dll
+    return _lib
+
+
+def knn_mean3(points: np.ndarray) -> np.ndarray:
+    """distCUDA2 value for every point of a (P, 3) float32 array (brute force, OpenMP)."""
+    pts = np.ascontiguousarray(points, dtype=np.float32)
+    out = np.empty(pts.shape[0], dtype=np.float32)
+    if pts.shape[0]:
+        lib().oracle_knn_mean3(pts.ctypes.data, pts.shape[0], out.ctypes.data)
+    return out
+
+
+def knn_mean3_subset(points: np.ndarray, idx: np.ndarray) -> np.ndarray:
+    """distCUDA2 value for the queries idx only (each against all points)."""
+    pts = np.ascontiguousarray(points, dtype=np.float32)
+    ii = np.ascontiguousarray(idx, dtype=np.int64)
+    out = np.empty(ii.shape[0], dtype=np.float32)
+    if ii.shape[0]:
+        lib().oracle_knn_mean3_subset(pts.ctypes.data, pts.shape[0], ii.ctypes.data, ii.shape[0], out.ctypes.data)
+    return out

@@ -88,11 +88,12 @@ def test_zero_gaussians_forward_backward(do_depth, render_geo):
         assert t.grad is not None and t.grad.shape == shape
 
 
-def test_nonempty_forward_surfaces_library_error(built_lib):
-    """P > 0 reaches the C ABI; with the kernels unbuilt it must raise, never fall back."""
+def test_nonempty_forward_refuses_host_tensors(built_lib):
+    """P > 0 host tensors are rejected before the C ABI: the kernels read device pointers, and
+    there is no CPU fallback."""
     s = settings()
     P = 4
-    with pytest.raises(RuntimeError, match="unsupported"):
+    with pytest.raises(RuntimeError, match="GPU tensor"):
         GaussianRasterizer(s)(torch.zeros(P, 3), torch.zeros(P, 3), torch.ones(P, 1), shs=torch.zeros(P, 16, 3),
                               scales=torch.ones(P, 3), rotations=torch.ones(P, 4), all_map=torch.zeros(P, 5))
 
@@ -117,9 +118,28 @@ def test_mark_visible_and_knn_empty():
     assert simple_knn._C.distCUDA2(torch.zeros(0, 3)).shape == (0,)
 
 
-def test_knn_nonempty_surfaces_library_error(built_lib):
-    with pytest.raises(RuntimeError, match="unsupported"):
+def test_knn_nonempty_refuses_host_tensors(built_lib):
+    with pytest.raises(RuntimeError, match="GPU tensor"):
         simple_knn._C.distCUDA2(torch.rand(8, 3))
+    with pytest.raises(RuntimeError, match="dimensions"):
+        simple_knn._C.distCUDA2(torch.rand(8, 2))
+
+
+def test_backward_hvar_is_a_module_attribute_not_thread_state():
+    """h_var of the covariance backward is read per call from _C.H_VAR_BWD (reference value 0.3,
+    backward.cu:211), so a value set on the training thread reaches autograd's device thread."""
+    import threading
+    assert _C.H_VAR_BWD == 0.3
+    seen = []
+    old = _C.H_VAR_BWD
+    try:
+        _C.H_VAR_BWD = 0.1
+        t = threading.Thread(target=lambda: seen.append(_C.H_VAR_BWD))
+        t.start()
+        t.join()
+    finally:
+        _C.H_VAR_BWD = old
+    assert seen == [0.1]
 
 
 def test_hierarchy_stub_raises():

@@ -1,0 +1,109 @@
+"""Binning primitives on the MI355X (hidegs_amd/csrc/primitives.hip) against generic integer
+oracles (oracle/binning.py).  Integer work: every result must be bit-identical."""
+import numpy as np
+import pytest
+import torch
+
+from hidegs_amd import primitives
+from oracle import binning
+
+pytestmark = pytest.mark.gpu
+
+
+def u64(a):
+    return torch.from_numpy(a.view(np.int64)).cuda()
+
+
+def u32(a):
+    return torch.from_numpy(a.view(np.int32)).cuda()
+
+
+def raster_like_keys(K, T, seed):
+    """(tile << 32) | float bits of a positive depth, Gaussian-major like duplicateWithKeys emits."""
+    g = np.random.default_rng(seed)
+    tiles = g.integers(0, T, K).astype(np.uint64)
+    depth = g.uniform(0.2, 100.0, K).astype(np.float32).view(np.uint32).astype(np.uint64)
+    return (tiles << np.uint64(32)) | depth, np.arange(K, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("K,T", [(32_768, 64), (400_000, 8160), (8_000_000, 8160), (4097, 32400), (1, 64), (2, 64)])
+def test_sort_raster_keys_bit_exact(K, T):
+    keys, vals = raster_like_keys(K, T, K)
+    end = 32 + primitives.higher_msb(T)
+    ko, vo = primitives.sort_pairs(u64(keys), u32(vals), 0, end)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, end)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+
+
+@pytest.mark.parametrize("begin,end", [(0, 64), (8, 40), (3, 17), (0, 0), (60, 64)])
+def test_sort_u64_bit_ranges_and_stability(begin, end):
+    g = np.random.default_rng(begin * 100 + end)
+    keys = g.integers(0, 2**63, 300_001, dtype=np.uint64) | (g.integers(0, 2, 300_001, dtype=np.uint64) << np.uint64(63))
+    keys[::7] = keys[3]  # many exact duplicates: stability is observable
+    vals = g.integers(0, 2**32, 300_001, dtype=np.uint64).astype(np.uint32)
+    ko, vo = primitives.sort_pairs(u64(keys), u32(vals), begin, end)
+    ek, ev = binning.stable_sort_pairs(keys, vals, begin, end)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+
+
+@pytest.mark.parametrize("n", [5, 4096, 123_457, 1_000_000])
+def test_sort_u32(n):
+    g = np.random.default_rng(n)
+    keys = g.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    keys[: n // 2] &= np.uint32(0xFF)  # skewed digits
+    vals = np.arange(n, dtype=np.uint32)
+    ko, vo = primitives.sort_pairs(u32(keys), u32(vals), 0, 32)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint32), ek)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+
+
+def test_sort_does_not_modify_inputs():
+    keys, vals = raster_like_keys(100_000, 8160, 1)
+    k, v = u64(keys), u32(vals)
+    k0, v0 = k.clone(), v.clone()
+    primitives.sort_pairs(k, v, 0, 45)
+    assert torch.equal(k, k0) and torch.equal(v, v0)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4095, 4096, 4097, 2_000_000, 10_000_003])
+def test_inclusive_scan_bit_exact(n):
+    g = np.random.default_rng(n)
+    x = g.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)  # large values: the sum wraps
+    got = primitives.inclusive_scan_u32(u32(x)).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, binning.inclusive_scan_u32(x))
+
+
+def test_inclusive_scan_tiles_touched_like_and_in_place():
+    g = np.random.default_rng(0)
+    x = g.integers(0, 9, 2_000_000).astype(np.uint32)  # tiles_touched-like counts
+    t = u32(x)
+    primitives.inclusive_scan_u32(t, out=t)  # in == out allowed
+    assert np.array_equal(t.cpu().numpy().view(np.uint32), binning.inclusive_scan_u32(x))
+
+
+@pytest.mark.parametrize("K,T", [(0, 10), (1, 10), (2, 10), (8_000_000, 8160), (50_000, 32400)])
+def test_tile_ranges_bit_exact(K, T):
+    keys, _ = raster_like_keys(K, T, 7)
+    keys = np.sort(keys)
+    got = primitives.identify_tile_ranges(u64(keys), T).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, binning.tile_ranges(keys, T))
+
+
+def test_binning_chain_scan_sort_ranges():
+    """scan(tiles_touched) -> offsets; pairs sorted over [0, 32+msb(T)); ranges cover every pair once."""
+    T, P = 8160, 200_000
+    g = np.random.default_rng(4)
+    touched = g.integers(0, 6, P).astype(np.uint32)
+    offsets = primitives.inclusive_scan_u32(u32(touched)).cpu().numpy().view(np.uint32)
+    K = int(offsets[-1])
+    keys, vals = raster_like_keys(K, T, 5)
+    ko, vo = primitives.sort_pairs(u64(keys), u32(vals), 0, 32 + primitives.higher_msb(T))
+    r = primitives.identify_tile_ranges(ko, T).cpu().numpy().astype(np.int64)
+    present = r[:, 1] > r[:, 0]
+    assert (r[present, 1] - r[present, 0]).sum() == K
+    tiles = (ko.cpu().numpy().view(np.uint64) >> np.uint64(32)).astype(np.int64)
+    for t in np.flatnonzero(present)[:50]:
+        assert (tiles[r[t, 0]:r[t, 1]] == t).all()

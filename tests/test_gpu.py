@@ -1,5 +1,6 @@
-"""GPU-box checks of what exists: the native library loads in a GPU process, the boundary
-never falls back to a CPU path, and the view-DP exchange runs over RCCL on device tensors."""
+"""GPU-box checks of the native library as a whole: it is the code that runs (mapped in the
+process, gfx950 kernels launched), it fails loudly where nothing is built, and the view-DP
+exchange runs over RCCL on device tensors."""
 import os
 import socket
 
@@ -10,15 +11,14 @@ pytestmark = pytest.mark.gpu
 
 
 def test_library_loaded_in_gpu_process(built_lib):
-    assert torch.cuda.is_available()
-    torch.zeros(1, device="cuda")  # initialise the HIP runtime first
-    from hidegs_amd import _lib
-    assert "hidegs" in _lib.version()
+    import simple_knn
+    simple_knn._C.distCUDA2(torch.rand(100, 3, device="cuda"))
+    torch.cuda.synchronize()
     maps = open(f"/proc/{os.getpid()}/maps").read()
     assert "libhidegs.so" in maps
 
 
-def test_boundary_raises_instead_of_falling_back(built_lib):
+def test_rasterizer_raises_instead_of_falling_back(built_lib):
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     d = "cuda"
     e = torch.empty(0, device=d)
