@@ -3,13 +3,24 @@
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL backend.)
 
-State ("Denials in force"): the rasterizer forward/backward is not built,
-so the metric is UNMEASURED and `value` is null -- nothing is estimated or faked.
-What does exist is measured for real:
-  * N > 1: the view-DP exchange step (hidegs_amd.view_dp) at the metric's size, 2M
-    Gaussians x 59 fp32 leaf-gradient values (472 MB) plus the densification statistics
-    and the visibility union, K timed steps after W warm-up steps, barrier +
-    synchronize on both sides, max over ranks.  Reported under "exchange".
+The headline metric needs the rasterizer forward + backward, whose kernels are not built
+("Decisions in force"), so `value` is null -- never estimated.  What the repo
+does build on this path is measured for real, at the configuration the metric is quoted
+on (config 3: 2M Gaussians, one 1920x1080 view, synthetic D2 inputs resident in HBM):
+
+  step      = the binning stage of one view: inclusive scan of the 2M tiles_touched,
+              stable radix sort of the K ~ 8M (tile|depth, id) pairs over bits
+              [0, 32 + getHigherMsb(8160)) = [0, 45), tile ranges (rasterizer_impl.cu:321-371).
+              W warm-up steps, then K timed steps between HIP events on the launch stream,
+              barrier + synchronize on both sides, max over ranks.
+  roofline  = the sort's scatter kernel (the dominant kernel of the step): 24 algorithmic
+              bytes per pair per launch (key 8 + value 4, read and written once), averaged
+              over its launches with per-launch HIP events (hidegs_kernel_timing), against
+              8 TB/s; traffic from the committed rocprofv3 PMC summary when present.
+  distCUDA2 = simple_knn._C.distCUDA2 on the 2M D2 centres (once-per-scene initialiser).
+  exchange  = the view-DP exchange of 2M x 59 fp32 leaf gradients + stats over RCCL
+              (a one-rank group at N = 1), HIP-event timed.
+  cpu_baseline = the oracle's stable sort (numpy, one core) on the same 8M pairs.
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -17,79 +28,199 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import platform
+import socket
+import subprocess
 import time
 
 N_GAUSSIANS = 2_000_000
 W_PX, H_PX = 1920, 1080
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+ROOT = os.path.dirname(os.path.abspath(__file__))
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03_traffic.json")
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def cpu_model() -> str:
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:  # noqa: BLE001
+        pass
+    return platform.processor() or "unknown"
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--knn-steps", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-exchange", action="store_true")
     args = ap.parse_args()
 
+    import numpy as np
     import torch
+    import torch.distributed as dist
+
+    import simple_knn
+    from hidegs_amd import _lib, primitives, synthetic
+    from hidegs_amd.view_dp import GradArena, ViewDPExchange
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if not dist.is_initialized():
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ["MASTER_PORT"] = str(free_port())
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+
+    def max_over_ranks(x: float) -> float:
+        t = torch.tensor([x], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t)
+
+    def timed(fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        dist.barrier()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()
+        for _ in range(steps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        dist.barrier()
+        wall = time.perf_counter() - t0
+        return max_over_ranks(e0.elapsed_time(e1) / steps), max_over_ranks(wall * 1e3 / steps)
+
+    # ---- the step: binning of one view (rank r renders its own view: seed r) -------------
+    wl = synthetic.binning_workload(N_GAUSSIANS, W_PX, H_PX, seed=rank, device=dev)
+    K, T = wl.num_pairs, wl.num_tiles
+    end_bit = 32 + primitives.higher_msb(T)
+    offsets = torch.empty_like(wl.tiles_touched)
+
+    def step():
+        primitives.inclusive_scan_u32(wl.tiles_touched, out=offsets)
+        ko, vo = primitives.sort_pairs(wl.keys, wl.values, 0, end_bit)
+        primitives.identify_tile_ranges(ko, T)
+
+    ms_step, wall_ms_step = timed(step, args.steps, args.warmup)
+
+    # per-kernel durations of the same step, live, with per-launch HIP events
+    kt_steps = max(10, min(args.steps, 50))
+    with _lib.kernel_timer() as kt:
+        for _ in range(kt_steps):
+            step()
+        torch.cuda.synchronize()
+        names = ["scan_reduce", "scan_small", "scan_downsweep", "radix_hist_u64", "radix_digit_scan",
+                 "radix_scatter_u64", "identify_ranges"]
+        kern = {}
+        for nm in names:
+            ms, n = kt.get(nm)
+            kern[nm] = {"avg_us": round(ms * 1e3 / max(n, 1), 2), "launches_per_step": n // kt_steps}
+    passes = kern["radix_scatter_u64"]["launches_per_step"]
+    scat_us = kern["radix_scatter_u64"]["avg_us"]
+    scat_bytes = 24 * K                            # per launch: read key+value, write key+value
+    achieved = scat_bytes / (scat_us * 1e-6) / 1e9
+    traffic = None
+    if os.path.exists(TRAFFIC_FILE):
+        with open(TRAFFIC_FILE) as f:
+            traffic = json.load(f).get("radix_scatter_u64", {}).get("hbm_bytes_per_launch")
+    sort_us = sum(kern[k]["avg_us"] * kern[k]["launches_per_step"]
+                  for k in ("radix_hist_u64", "radix_digit_scan", "radix_scatter_u64"))
 
     line = {
         "metric": "fwd+bwd iters/sec & HBM GB/s at 2M Gaussians, 1920x1080",
         "value": None,
         "unit": "iters/s",
-        "n_gpus": args.gpus,
+        "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": None,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic",
-        "config": {"workload": "config 3: 2M Gaussians, 1920x1080, fwd+bwd", "n_gaussians": N_GAUSSIANS,
-                   "width": W_PX, "height": H_PX, "parallelism": f"view-dp{max(world, 1)}"},
-        "status": "UNMEASURED: the rasterizer forward/backward is not built (DESIGN.md, 'Denials in force')",
-        "roofline": None,
+        "dtype": "u64/u32 (binning), f32 (distCUDA2, exchange)",
+        "data": "synthetic (SURVEY §8(d) D2, seeded per rank)",
+        "config": {"workload": "config 3: 2M Gaussians, 1920x1080, one view per rank -- binning stage, "
+                               "distCUDA2 and the view-DP exchange measured; rasterizer fwd/bwd not built",
+                   "n_gaussians": N_GAUSSIANS, "width": W_PX, "height": H_PX, "tiles": T, "pairs_K": K,
+                   "sort_bits": [0, end_bit], "parallelism": f"view-dp{world}"},
+        "status": "headline UNMEASURED: the rasterizer forward/backward kernels are not built "
+                  "(DESIGN.md, 'Decisions in force'); value stays null",
+        "binning_step": {"ms_per_step": round(ms_step, 4), "wall_ms_per_step": round(wall_ms_step, 4),
+                         "pairs_per_s_all_ranks": K * world / (ms_step * 1e-3),
+                         "views_per_s_all_ranks": world / (ms_step * 1e-3),
+                         "sort_passes": passes, "sort_us": round(sort_us, 2), "kernels": kern},
+        "roofline": {"kernel": "radix_scatter_u64", "bound": "hbm", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": traffic, "algorithmic_bytes_per_launch": scat_bytes,
+                     "avg_launch_us": scat_us},
         "cpu_baseline": None,
     }
 
-    if world > 1:
-        import torch.distributed as dist
-        from hidegs_amd.view_dp import LEAF_WIDTHS, ViewDPExchange
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        dev = torch.device("cuda", local)
+    # ---- distCUDA2 at 2M ---------------------------------------------------------------------
+    pts = synthetic.frustum_points(N_GAUSSIANS, seed=rank).to(dev)
+    knn_ms, _ = timed(lambda: simple_knn._C.distCUDA2(pts), args.knn_steps, 1)
+    with _lib.kernel_timer() as kt:
+        simple_knn._C.distCUDA2(pts)
+        torch.cuda.synchronize()
+        kk = {nm: round(kt.get(nm)[0] * 1e3, 1) for nm in ("bounds", "morton", "radix_scatter_u64", "gather",
+                                                             "leaf_box", "knn_leaf", "knn_hard")}
+    line["distCUDA2"] = {"points": N_GAUSSIANS, "ms": round(knn_ms, 3),
+                         "points_per_s_all_ranks": N_GAUSSIANS * world / (knn_ms * 1e-3), "kernels_us": kk,
+                         "algorithmic_bytes": 16 * N_GAUSSIANS,
+                         "hbm_frac": round(16 * N_GAUSSIANS / (knn_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
+
+    # ---- view-DP exchange at 2M ---------------------------------------------------------------
+    if not args.no_exchange:
         g = torch.Generator(device=dev).manual_seed(rank)
-        visible = torch.ones(N_GAUSSIANS, dtype=torch.bool, device=dev)  # synthetic D2 views see ~all Gaussians
-        grads = {k: torch.randn(N_GAUSSIANS, w, device=dev, generator=g) for k, w in LEAF_WIDTHS.items()}
-        gmax = torch.rand(N_GAUSSIANS, device=dev, generator=g)
-        rmax = torch.rand(N_GAUSSIANS, device=dev, generator=g)
-        denom = torch.ones(N_GAUSSIANS, device=dev)
+        visible = torch.rand(N_GAUSSIANS, device=dev, generator=g) < 0.9
+        arena = GradArena(N_GAUSSIANS, device=dev)
+        arena.flat.normal_(generator=g)
+        norm = torch.rand(N_GAUSSIANS, 1, device=dev, generator=g)
+        radii = torch.rand(N_GAUSSIANS, device=dev, generator=g)
         ex = ViewDPExchange()
-
-        def step():
-            ex.exchange(grads, visible, max_stats=[gmax, rmax], sum_stats=[denom])
-
-        for _ in range(args.warmup):
-            step()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        dist.barrier()
-        dt = torch.tensor([time.perf_counter() - t0], device=dev)
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        ms = float(dt) * 1e3 / max(args.steps, 1)
-        payload = ex.last.reduced_bytes
-        line["exchange"] = {"ms_per_step": ms, "grad_bytes_per_rank": payload,
-                            "algbw_GBps": payload / (ms * 1e-3) / 1e9, "collectives_per_step": ex.last.collectives,
+        ex_ms, _ = timed(lambda: ex.exchange(arena, visible, max_stats=[norm, radii]), 20, 3)
+        line["exchange"] = {"ms_per_step": round(ex_ms, 3), "world": world, "grad_bytes_per_rank": ex.last.reduced_bytes,
+                            "algbw_GBps": ex.last.reduced_bytes / (ex_ms * 1e-3) / 1e9,
+                            "collectives_per_step": ex.last.collectives, "compacted": ex.last.compacted,
                             "union_rows": ex.last.union_rows}
-        dist.destroy_process_group()
 
+    # ---- CPU baseline (rank 0, N = 1): the oracle's stable sort on the same pairs -------------
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import binning
+        keys = wl.keys.cpu().numpy().view(np.uint64)
+        vals = wl.values.cpu().numpy().view(np.uint32)
+        reps, t0 = 0, time.perf_counter()
+        while reps < 3 or (time.perf_counter() - t0 < 10.0 and reps < 20):
+            binning.stable_sort_pairs(keys, vals, 0, end_bit)
+            reps += 1
+        dt = (time.perf_counter() - t0) / reps
+        line["cpu_baseline"] = {"value": K / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+                                "sample": f"stable sort of the same {K} (key, value) pairs over bits [0,{end_bit}) "
+                                          f"(numpy argsort kind=stable + gather, oracle/binning.py), {reps} reps",
+                                "cpu": cpu_model(), "gpu_speedup_sort": round(dt * 1e3 / (sort_us * 1e-3), 1)}
+
+    dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(line), flush=True)
 

@@ -54,6 +54,9 @@ SIGNATURES = {
     "hidegs_sort_pairs_u32": (I, [P, SZ, P, P, P, P, LL, I, I, P]),
     "hidegs_identify_tile_ranges": (I, [P, LL, P, I, P]),
     "hidegs_higher_msb": (U32, [U32]),
+    "hidegs_kernel_timing": (None, [I]),
+    "hidegs_kernel_timing_reset": (None, []),
+    "hidegs_kernel_time": (I, [C.c_char_p, P, P]),
     "hidegs_last_error": (C.c_char_p, []),
     "hidegs_version": (C.c_char_p, []),
 }
@@ -161,3 +164,25 @@ def check_with(rc: int, what: str, *scratches: "Scratch") -> None:
         if cause is not None:
             raise e from cause
         raise
+
+
+class kernel_timer:
+    """Context manager: per-kernel device times (ms, launches) of this library's kernels.
+
+    with kernel_timer() as kt: ...;  kt.get("radix_scatter_u64") -> (total_ms, launches)
+    """
+
+    def __enter__(self):
+        lib().hidegs_kernel_timing_reset()
+        lib().hidegs_kernel_timing(1)
+        return self
+
+    def __exit__(self, *exc):
+        lib().hidegs_kernel_timing(0)
+        return False
+
+    @staticmethod
+    def get(name: str):
+        ms, n = C.c_double(0.0), C.c_longlong(0)
+        lib().hidegs_kernel_time(name.encode(), C.byref(ms), C.byref(n))
+        return ms.value, n.value

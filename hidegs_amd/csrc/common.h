@@ -82,3 +82,29 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
 }
 
 }  // namespace hidegs
+
+namespace hidegs {
+
+// Per-kernel device timing (hidegs_kernel_timing in include/hidegs.h): when enabled, each
+// launch made through HIDEGS_LAUNCH is bracketed by two hipEvents recorded on its stream;
+// the durations are resolved and accumulated per kernel name when they are queried.
+bool kernel_timing_enabled();
+struct LaunchTimer {
+    const char* name;
+    hipStream_t stream;
+    hipEvent_t start = nullptr, stop = nullptr;
+    LaunchTimer(const char* n, hipStream_t s);
+    ~LaunchTimer();
+};
+
+}  // namespace hidegs
+
+#define HIDEGS_LAUNCH(NAME, KERNEL, GRID, BLOCK, SHMEM, STREAM, ...)                        \
+    do {                                                                                   \
+        if (::hidegs::kernel_timing_enabled()) {                                           \
+            ::hidegs::LaunchTimer _t(NAME, STREAM);                                        \
+            hipLaunchKernelGGL(KERNEL, GRID, BLOCK, SHMEM, STREAM, __VA_ARGS__);           \
+        } else {                                                                           \
+            hipLaunchKernelGGL(KERNEL, GRID, BLOCK, SHMEM, STREAM, __VA_ARGS__);           \
+        }                                                                                  \
+    } while (0)

@@ -475,20 +475,20 @@ int dist_cuda2(hidegs_alloc_fn alloc, void* user, int P, const float* points, fl
 
     if (hipMemsetAsync(l.counters, 0, sizeof(KnnCounters), stream) != hipSuccess)
         return fail(HIDEGS_E_HIP, "distCUDA2: memset failed");
-    hipLaunchKernelGGL(bounds_kernel, dim3(nbound), dim3(kBlock), 0, stream, points, P, l.partials);
-    hipLaunchKernelGGL(bounds_finalize_kernel, dim3(1), dim3(kBlock), 0, stream, l.partials, nbound, l.params);
-    hipLaunchKernelGGL(morton_kernel, dim3(nb), dim3(kBlock), 0, stream, points, P, l.params, l.keys, l.vals);
+    HIDEGS_LAUNCH("bounds", bounds_kernel, dim3(nbound), dim3(kBlock), 0, stream, points, P, l.partials);
+    HIDEGS_LAUNCH("bounds_finalize", bounds_finalize_kernel, dim3(1), dim3(kBlock), 0, stream, l.partials, nbound, l.params);
+    HIDEGS_LAUNCH("morton", morton_kernel, dim3(nb), dim3(kBlock), 0, stream, points, P, l.params, l.keys, l.vals);
     int rc = sort_pairs_u64(l.sort_tmp, l.sort_bytes, l.keys, l.keys_sorted, l.vals, l.vals_sorted, P, 0,
                             3 * kMortonBits, stream);
     if (rc) return rc;
-    hipLaunchKernelGGL(gather_kernel, dim3(nb), dim3(kBlock), 0, stream, points, l.vals_sorted, P, l.sp);
-    hipLaunchKernelGGL(leaf_box_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P, nleaves,
+    HIDEGS_LAUNCH("gather", gather_kernel, dim3(nb), dim3(kBlock), 0, stream, points, l.vals_sorted, P, l.sp);
+    HIDEGS_LAUNCH("leaf_box", leaf_box_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P, nleaves,
                        l.leaves);
-    hipLaunchKernelGGL(super_box_kernel, dim3(ceil_div(nsuper, kWaves)), dim3(kBlock), 0, stream, l.leaves, nleaves,
+    HIDEGS_LAUNCH("super_box", super_box_kernel, dim3(ceil_div(nsuper, kWaves)), dim3(kBlock), 0, stream, l.leaves, nleaves,
                        nsuper, l.supers);
-    hipLaunchKernelGGL(knn_leaf_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P, nleaves,
+    HIDEGS_LAUNCH("knn_leaf", knn_leaf_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P, nleaves,
                        nsuper, l.leaves, l.supers, mean_dists, l.hard, l.counters);
-    hipLaunchKernelGGL(knn_hard_kernel, dim3(std::min(2048, ceil_div(nleaves, kWaves))), dim3(kBlock), 0, stream, l.sp,
+    HIDEGS_LAUNCH("knn_hard", knn_hard_kernel, dim3(std::min(2048, ceil_div(nleaves, kWaves))), dim3(kBlock), 0, stream, l.sp,
                        P, nleaves, nsuper, l.leaves, l.supers, mean_dists, l.hard, l.counters);
     return check_launch("distCUDA2", stream, 0);
 }

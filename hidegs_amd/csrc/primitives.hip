@@ -421,9 +421,9 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         const bool to_out = ((passes - 1 - p) % 2) == 0;
         K* dk = to_out ? keys_out : alt_k;
         uint32_t* dv = to_out ? vals_out : alt_v;
-        hipLaunchKernelGGL(radix_hist_kernel<K>, dim3(nt), dim3(kBlock), 0, stream, src_k, n, shift, mask, nt, counts);
-        hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(kRadix), dim3(kBlock), 0, stream, counts, nt, totals);
-        hipLaunchKernelGGL(radix_scatter_kernel<K>, dim3(nt), dim3(kBlock), 0, stream, src_k, src_v, dk, dv, n, shift,
+        HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_hist_u64" : "radix_hist_u32"), radix_hist_kernel<K>, dim3(nt), dim3(kBlock), 0, stream, src_k, n, shift, mask, nt, counts);
+        HIDEGS_LAUNCH("radix_digit_scan", radix_digit_scan_kernel, dim3(kRadix), dim3(kBlock), 0, stream, counts, nt, totals);
+        HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"), radix_scatter_kernel<K>, dim3(nt), dim3(kBlock), 0, stream, src_k, src_v, dk, dv, n, shift,
                            mask, nt, counts, totals);
         src_k = dk;
         src_v = dv;
@@ -443,9 +443,9 @@ int inclusive_scan_u32(void* scratch, size_t scratch_bytes, const uint32_t* in, 
     const int nt = ceil_div(n, kTile);
     Carver c(scratch);
     uint32_t* sums = c.take<uint32_t>(nt);
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3(nt), dim3(kBlock), 0, stream, in, n, sums);
-    hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(kBlock), 0, stream, sums, nt, (uint32_t*)nullptr);
-    hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nt), dim3(kBlock), 0, stream, in, n, sums, out);
+    HIDEGS_LAUNCH("scan_reduce", scan_reduce_kernel, dim3(nt), dim3(kBlock), 0, stream, in, n, sums);
+    HIDEGS_LAUNCH("scan_small", scan_small_kernel, dim3(1), dim3(kBlock), 0, stream, sums, nt, (uint32_t*)nullptr);
+    HIDEGS_LAUNCH("scan_downsweep", scan_downsweep_kernel, dim3(nt), dim3(kBlock), 0, stream, in, n, sums, out);
     return check_launch("inclusive_scan_u32", stream, 0);
 }
 
@@ -472,7 +472,7 @@ int identify_tile_ranges(const uint64_t* keys, long long n, uint32_t* ranges, in
         return fail(HIDEGS_E_HIP, "identify_tile_ranges: memset failed");
     if (n == 0) return check_launch("identify_tile_ranges", stream, 0);
     if (!keys) return fail(HIDEGS_E_ARG, "identify_tile_ranges: NULL keys");
-    hipLaunchKernelGGL(identify_ranges_kernel, dim3(ceil_div(n, kBlock)), dim3(kBlock), 0, stream, keys, n,
+    HIDEGS_LAUNCH("identify_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock)), dim3(kBlock), 0, stream, keys, n,
                        reinterpret_cast<uint2*>(ranges), (uint32_t)num_tiles);
     return check_launch("identify_tile_ranges", stream, 0);
 }

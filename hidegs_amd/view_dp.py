@@ -1,35 +1,45 @@
-"""View-data-parallel gradient exchange for multi-GPU HiDeGS training.
+"""View-data-parallel exchange for multi-GPU HiDeGS training.
 
 The reference is single-process; this is a new capability.  Every rank
 holds a full replica of the Gaussian parameters and renders its own camera view
-(`view_index(step, rank, world)`); after the backward pass one exchange step makes
-the replicas agree again:
+(`view_index(step, rank, world)`); after the backward pass one exchange step makes the
+replicas agree again, with the result the reference would reach by processing the
+world's views one after another:
 
-    leaf gradients (xyz, f_dc, f_rest, opacity, scaling, rotation)  SUM
-    densification statistics kept as running maxima                 MAX
-      (viewspace-gradient norm, scene/gaussian_model.py:763-765; max_radii2D)
-    densification counters (denom)                                   SUM
-    visibility masks                                                 OR
+    leaf gradients (xyz, f_dc, f_rest, opacity, scaling, rotation)   SUM
+    per-step densification maxima (|dL/dmeans2D| norm, radii)        MAX, one collective
+    per-Gaussian count of views that saw it (the denom increment)    from the masks
+    visibility                                                       OR
 
-Compaction: gradients of Gaussians that no rank saw are zero on every rank (the
-rasterizer writes zero rows for invisible Gaussians), so only the union-visible rows
-are packed and reduced; the result equals the dense all-reduce exactly.  The union is
-formed from 1-bit masks gathered from every rank (N/8 bytes each).  Packed rows are
-reduced in flat fp32 buckets of `bucket_bytes` (default 64 MiB), all issued
-asynchronously, because a ring over xGMI is per-link bound (~153 GB/s) and pays a
-fixed cost per collective: few, large collectives.
+`add_densification_stats` keeps a running max of the view-space gradient norm and
+counts views in `denom` (scene/gaussian_model.py:763-765).  Both accumulators are
+replicated, so only this step's contributions are exchanged: the MAX of the per-step
+norms and the number of ranks whose view saw each Gaussian.  Summing the accumulators
+themselves would count the replicated history `world` times per step.
 
-Backend: whatever process group is current -- "nccl" (RCCL on ROCm) on the GPU,
-"gloo" in the CPU tests.  Bitwise OR is done by gathering packed masks (RCCL has no
-bitwise reduction).
+Leaf gradients live in one flat fp32 arena (`GradArena`), field-major, so each
+parameter's `.grad` is a contiguous view that autograd accumulates into in place and the
+dense exchange is an in-place all-reduce of the arena with no copies.  When few rows are
+visible anywhere (union fraction below `compact_below`) only those rows are packed and
+reduced; rows outside the union are zero on every rank (the rasterizer's backward writes
+zero rows for Gaussians it did not render), so the packed sum equals the dense one.
+Buckets of `bucket_bytes` (default 64 MiB) are all issued before any is waited on: a ring
+over xGMI is bound per link (~153 GB/s) and pays a fixed cost per collective.
+
+Backend: whatever process group is current -- "nccl" (RCCL on ROCm) on the GPU, "gloo" in
+the CPU tests.  Bitwise OR is formed from an all-gather of packed masks (RCCL has no
+bitwise reduction), which also yields the per-Gaussian view count.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, Iterable, List, Optional
+from typing import Dict, Iterable, List, Optional, Union
 
 import torch
 import torch.distributed as dist
+
+LEAF_WIDTHS = {"xyz": 3, "f_dc": 3, "f_rest": 45, "opacity": 1, "scaling": 3, "rotation": 4}
+"""Per-Gaussian fp32 widths of the HiDeGS leaf parameters (59 floats = 236 B; SURVEY §8(e) E1)."""
 
 _BITS = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8)
 
@@ -50,9 +60,41 @@ def pack_mask(mask: torch.Tensor) -> torch.Tensor:
 
 
 def unpack_mask(bits: torch.Tensor, n: int) -> torch.Tensor:
-    """Inverse of pack_mask."""
-    b = bits.reshape(-1, 1) & _BITS.to(bits.device)
-    return (b != 0).reshape(-1)[:n]
+    """Inverse of pack_mask (also accepts a (R, B) stack, giving (R, n))."""
+    b = bits.unsqueeze(-1) & _BITS.to(bits.device)
+    return (b != 0).reshape(*bits.shape[:-1], -1)[..., :n]
+
+
+class GradArena:
+    """One flat fp32 buffer holding every leaf gradient, field-major ([field][row][col]).
+
+    `views[name]` is a contiguous (n, width) view; `attach` makes it the `.grad` of a
+    parameter (autograd then accumulates into it in place, shape-matched via view_as).
+    """
+
+    def __init__(self, n: int, widths: Dict[str, int] = None, device=None, dtype=torch.float32):
+        self.n = int(n)
+        self.widths = dict(widths or LEAF_WIDTHS)
+        self.row_width = sum(self.widths.values())
+        self.flat = torch.zeros(self.n * self.row_width, dtype=dtype, device=device)
+        self.views: Dict[str, torch.Tensor] = {}
+        off = 0
+        for name, w in self.widths.items():
+            self.views[name] = self.flat[off:off + self.n * w].view(self.n, w)
+            off += self.n * w
+
+    def attach(self, params: Dict[str, torch.Tensor]) -> None:
+        for name, p in params.items():
+            v = self.views[name]
+            if p.numel() != v.numel():
+                raise ValueError(f"{name}: parameter has {p.numel()} values, arena slot {v.numel()}")
+            p.grad = v.view_as(p)
+
+    def zero_(self) -> None:
+        self.flat.zero_()
+
+    def __getitem__(self, name: str) -> torch.Tensor:
+        return self.views[name]
 
 
 @dataclass
@@ -60,110 +102,152 @@ class ExchangeStats:
     union_rows: int = 0
     reduced_bytes: int = 0
     collectives: int = 0
+    compacted: bool = False
+
+
+@dataclass
+class ExchangeResult:
+    union: torch.Tensor       # bool (N,): visible in some rank's view (the masked Adam's rows)
+    view_count: torch.Tensor  # float32 (N, 1): how many ranks' views saw each Gaussian (denom increment)
 
 
 class ViewDPExchange:
     """One exchange step per training iteration of view-data-parallel rendering."""
 
     def __init__(self, group: Optional[dist.ProcessGroup] = None, bucket_bytes: int = 64 << 20,
-                 compact: bool = True):
+                 compact_below: float = 0.75, debug: bool = False):
         if bucket_bytes < 4:
             raise ValueError("bucket_bytes must hold at least one fp32 value")
+        if not 0.0 <= compact_below <= 1.0:
+            raise ValueError("compact_below is a fraction of rows in [0, 1]")
         self.group = group
         self.bucket_bytes = int(bucket_bytes)
-        self.compact = compact
+        self.compact_below = float(compact_below)
+        self.debug = debug
         self.last = ExchangeStats()
 
     # ---- visibility -------------------------------------------------------------
-    def union_visibility(self, visible: torch.Tensor) -> torch.Tensor:
-        """OR of the (N,) bool masks of every rank."""
+    def gather_visibility(self, visible: torch.Tensor):
+        """(union bool (N,), view_count float32 (N,1)) over every rank's mask; one all-gather."""
+        if visible.dtype != torch.bool or visible.dim() != 1:
+            raise ValueError("visible must be a 1-D bool mask")
         world = dist.get_world_size(self.group)
         bits = pack_mask(visible)
         flat = bits.new_empty((world * bits.numel(),))
         dist.all_gather_into_tensor(flat, bits, group=self.group)
-        out = flat.view(world, bits.numel())
         self.last.collectives += 1
-        merged = out[0].clone()
-        for r in range(1, world):
-            merged |= out[r]
-        return unpack_mask(merged, visible.numel())
+        per_rank = unpack_mask(flat.view(world, bits.numel()), visible.numel())
+        count = per_rank.sum(0, dtype=torch.int32)
+        return count > 0, count.to(torch.float32).unsqueeze(1)
 
     # ---- leaf gradients -----------------------------------------------------------
-    def _reduce_flat(self, flat: torch.Tensor) -> None:
+    def _all_reduce_buckets(self, flat: torch.Tensor) -> None:
         per = max(1, self.bucket_bytes // flat.element_size())
-        works = []
-        for start in range(0, flat.numel(), per):
-            works.append(dist.all_reduce(flat[start:start + per], op=dist.ReduceOp.SUM, group=self.group,
-                                         async_op=True))
+        works = [dist.all_reduce(flat[s:s + per], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                 for s in range(0, flat.numel(), per)]
         for w in works:
             w.wait()
         self.last.collectives += len(works)
         self.last.reduced_bytes += flat.numel() * flat.element_size()
 
-    def sum_gradients(self, grads: Iterable[torch.Tensor], union: Optional[torch.Tensor] = None) -> None:
+    def sum_gradients(self, grads: Union[GradArena, Iterable[torch.Tensor]],
+                      union: Optional[torch.Tensor] = None) -> None:
         """In-place SUM over ranks of per-Gaussian gradients (each (N, ...), same N).
 
-        With `union` (bool (N,), identical on every rank) only those rows are packed and
-        reduced; rows outside it must be zero on every rank.
+        `union` (bool (N,), identical on every rank, rows visible to some rank) allows the
+        compacted exchange; every row outside it must be zero on every rank.
         """
-        grads = [g for g in grads if g is not None]
-        if not grads:
-            return
-        n = grads[0].size(0)
-        for g in grads:
+        if isinstance(grads, GradArena):
+            tensors, n = list(grads.views.values()), grads.n
+            arena = grads.flat
+        else:
+            tensors = [g for g in grads if g is not None]
+            if not tensors:
+                return
+            n, arena = tensors[0].size(0), None
+        for g in tensors:
             if g.size(0) != n:
                 raise ValueError("all gradients must have the same number of rows")
             if g.dtype != torch.float32:
                 raise ValueError("gradients are exchanged in fp32")
             if not g.is_contiguous():
                 raise ValueError("gradients must be contiguous (results are written back in place)")
+        if union is not None:
+            if union.dtype != torch.bool or union.dim() != 1 or union.numel() != n:
+                raise ValueError(f"union must be a bool mask of the {n} gradient rows "
+                                 "(fullP rows: scatter hierarchy render_indices/parent_indices into it)")
         rows = None
-        if union is not None and self.compact:
-            rows = union.nonzero().flatten()
-            self.last.union_rows = rows.numel()
-            if rows.numel() == 0:
-                return
+        if union is not None and n:
+            nu = int(union.sum())
+            self.last.union_rows = nu
+            if nu < self.compact_below * n:
+                rows = union.nonzero().flatten()
+            if self.debug:
+                outside = ~union
+                for g in tensors:
+                    if bool(g.reshape(n, -1)[outside].ne(0).any()):
+                        raise RuntimeError("view-DP: a gradient row outside the visibility union is non-zero; "
+                                           "the compacted exchange would desynchronise the replicas")
         else:
             self.last.union_rows = n
-        widths = [g[0].numel() if n else 0 for g in grads]
-        parts = [(g.reshape(n, -1) if rows is None else g.reshape(n, -1).index_select(0, rows)) for g in grads]
-        flat = torch.cat([p.reshape(-1) for p in parts])
-        self._reduce_flat(flat)
-        nr = n if rows is None else rows.numel()
-        off = 0
-        for g, w in zip(grads, widths):
-            block = flat[off:off + nr * w].view(nr, w)
-            off += nr * w
-            if rows is None:
-                g.reshape(n, -1).copy_(block)
+        if rows is None:
+            self.last.compacted = False
+            if arena is not None:
+                self._all_reduce_buckets(arena)
             else:
-                g.reshape(n, -1).index_copy_(0, rows, block)
+                flat = torch.cat([g.reshape(-1) for g in tensors])
+                self._all_reduce_buckets(flat)
+                off = 0
+                for g in tensors:
+                    g.view(-1).copy_(flat[off:off + g.numel()])
+                    off += g.numel()
+            return
+        self.last.compacted = True
+        if rows.numel() == 0:
+            return
+        widths = [g[0].numel() for g in tensors]
+        packed = torch.empty(rows.numel() * sum(widths), dtype=torch.float32, device=tensors[0].device)
+        off = 0
+        for g, w in zip(tensors, widths):
+            torch.index_select(g.reshape(n, w), 0, rows, out=packed[off:off + rows.numel() * w].view(-1, w))
+            off += rows.numel() * w
+        self._all_reduce_buckets(packed)
+        off = 0
+        for g, w in zip(tensors, widths):
+            g.reshape(n, w).index_copy_(0, rows, packed[off:off + rows.numel() * w].view(-1, w))
+            off += rows.numel() * w
 
     # ---- statistics ---------------------------------------------------------------
-    def max_stats(self, stats: Iterable[torch.Tensor]) -> None:
+    def max_stats(self, stats: List[torch.Tensor]) -> None:
+        """In-place MAX over ranks of per-step maxima, all in ONE collective."""
+        stats = [s for s in stats if s is not None]
+        if not stats:
+            return
+        flat = torch.cat([s.reshape(-1).to(torch.float32) for s in stats])
+        dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=self.group)
+        self.last.collectives += 1
+        off = 0
         for s in stats:
-            if s is not None:
-                dist.all_reduce(s, op=dist.ReduceOp.MAX, group=self.group)
-                self.last.collectives += 1
-
-    def sum_stats(self, stats: Iterable[torch.Tensor]) -> None:
-        for s in stats:
-            if s is not None:
-                dist.all_reduce(s, op=dist.ReduceOp.SUM, group=self.group)
-                self.last.collectives += 1
+            s.view(-1).copy_(flat[off:off + s.numel()].to(s.dtype))
+            off += s.numel()
 
     # ---- the whole exchange step ----------------------------------------------------
-    def exchange(self, grads: Dict[str, torch.Tensor], visible: torch.Tensor,
-                 max_stats: Optional[List[torch.Tensor]] = None,
-                 sum_stats: Optional[List[torch.Tensor]] = None) -> torch.Tensor:
-        """Run one exchange step; returns the union visibility mask (for the masked Adam)."""
+    def exchange(self, grads: Union[GradArena, Dict[str, torch.Tensor]], visible: torch.Tensor,
+                 max_stats: Optional[List[torch.Tensor]] = None) -> ExchangeResult:
+        """Run one exchange step.
+
+        grads      GradArena or {name: (N, w) grad}; summed in place.
+        visible    this rank's visibility filter (radii > 0), bool (N,).
+        max_stats  this step's per-Gaussian maxima (e.g. the view-space gradient norm of
+                   visible rows, radii), reduced in place by MAX.
+        Returns the union mask and the per-Gaussian view count; the caller then applies the
+        reference's update to its replicated accumulators:
+            xyz_gradient_accum = max(xyz_gradient_accum, norm)   # on union rows
+            denom += view_count
+        """
         self.last = ExchangeStats()
-        union = self.union_visibility(visible)
-        self.sum_gradients(grads.values(), union if self.compact else None)
+        union, count = self.gather_visibility(visible)
+        g = grads if isinstance(grads, GradArena) else grads.values()
+        self.sum_gradients(g, union)
         self.max_stats(max_stats or [])
-        self.sum_stats(sum_stats or [])
-        return union
-
-
-LEAF_WIDTHS = {"xyz": 3, "f_dc": 3, "f_rest": 45, "opacity": 1, "scaling": 3, "rotation": 4}
-"""Per-Gaussian fp32 widths of the HiDeGS leaf parameters (59 floats = 236 B; SURVEY §8(e) E1)."""
+        return ExchangeResult(union, count)

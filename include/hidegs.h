@@ -139,6 +139,16 @@ int hidegs_identify_tile_ranges(const uint64_t* sorted_keys, long long n, uint32
 /* [host] getHigherMsb: bits needed to hold n, at least 1; the sort end bit is 32 + this of the tile count. */
 uint32_t hidegs_higher_msb(uint32_t n);
 
+/*
+ * [host] Per-kernel device timing.  While enabled, every kernel this library launches is
+ * bracketed by two hipEvents on its stream (a few microseconds of overhead per launch);
+ * hidegs_kernel_time resolves them and returns the accumulated milliseconds and launch
+ * count for one kernel name (e.g. "radix_scatter_u64", "knn_leaf"), -1 if it never ran.
+ */
+void hidegs_kernel_timing(int enable);
+void hidegs_kernel_timing_reset(void);
+int hidegs_kernel_time(const char* name, double* total_ms, long long* launches);
+
 const char* hidegs_last_error(void);
 const char* hidegs_version(void);
 

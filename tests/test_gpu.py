@@ -49,9 +49,11 @@ def test_view_dp_exchange_over_rccl_single_rank():
         grads = {k: torch.randn(n, w, device="cuda", generator=g) * visible[:, None] for k, w in LEAF_WIDTHS.items()}
         ref = {k: v.clone() for k, v in grads.items()}
         gmax = torch.rand(n, device="cuda", generator=g)
-        union = ViewDPExchange(bucket_bytes=1 << 20).exchange(grads, visible, max_stats=[gmax.clone()])
+        res = ViewDPExchange(bucket_bytes=1 << 20, compact_below=1.0).exchange(grads, visible,
+                                                                                max_stats=[gmax.clone()])
         torch.cuda.synchronize()
-        assert torch.equal(union, visible)
+        assert torch.equal(res.union, visible)
+        assert torch.equal(res.view_count.squeeze(1), visible.float())
         for k in grads:
             assert torch.equal(grads[k], ref[k])
     finally:

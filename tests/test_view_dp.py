@@ -1,9 +1,11 @@
 """View-data-parallel exchange over gloo, world sizes 2 and 3, on CPU.
 
 Each rank builds synthetic per-view gradients with its own visibility mask (rows a view
-does not see are zero, as the rasterizer's backward produces them), runs one exchange
-step and checks the result against the sum / max / OR computed locally from every
-rank's regenerated inputs.
+does not see are zero, as the rasterizer's backward produces them), runs the exchange for
+several steps starting from non-zero replicated densification state, and checks the
+replicas against the reference's sequential semantics: processing the world's views one
+after another with add_densification_stats (scene/gaussian_model.py:763-765):
+    accum = max(accum, norm_v) on rows view v sees;  denom += 1 on those rows.
 """
 import os
 import socket
@@ -13,23 +15,28 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from hidegs_amd.view_dp import LEAF_WIDTHS, ViewDPExchange, pack_mask, unpack_mask, view_index
+from hidegs_amd.view_dp import (LEAF_WIDTHS, GradArena, ViewDPExchange, pack_mask, unpack_mask, view_index)
 
 N = 1000
+STEPS = 3
 
 
-def rank_inputs(rank, n=N):
-    g = torch.Generator().manual_seed(1234 + rank)
+def rank_inputs(rank, step, n=N):
+    g = torch.Generator().manual_seed(1234 + 97 * rank + 7919 * step)
     visible = torch.rand(n, generator=g) < (0.3 + 0.1 * rank)
     grads = {}
     for name, w in LEAF_WIDTHS.items():
         t = torch.randn(n, w, generator=g)
         t[~visible] = 0.0
         grads[name] = t
-    grad_norm_max = torch.rand(n, generator=g) * visible
-    max_radii = (torch.rand(n, generator=g) * 10).floor() * visible
-    denom = visible.float()
-    return visible, grads, grad_norm_max, max_radii, denom
+    norm = torch.rand(n, 1, generator=g) * visible[:, None]
+    radii = (torch.rand(n, generator=g) * 10).floor() * visible
+    return visible, grads, norm, radii
+
+
+def initial_state(n=N):
+    g = torch.Generator().manual_seed(5)
+    return torch.rand(n, 1, generator=g), (torch.rand(n, 1, generator=g) * 4).floor(), torch.rand(n, generator=g) * 3
 
 
 def free_port():
@@ -40,39 +47,56 @@ def free_port():
     return port
 
 
-def worker(rank, world, port, compact, bucket_bytes, q):
+def worker(rank, world, port, compact_below, bucket_bytes, use_arena, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        visible, grads, gmax, rmax, denom = rank_inputs(rank)
-        ex = ViewDPExchange(bucket_bytes=bucket_bytes, compact=compact)
-        union = ex.exchange(grads, visible, max_stats=[gmax, rmax], sum_stats=[denom])
-        # expected values from every rank's regenerated inputs
-        all_in = [rank_inputs(r) for r in range(world)]
-        exp_union = torch.zeros(N, dtype=torch.bool)
-        for v, *_ in all_in:
-            exp_union |= v
-        err = 0.0
-        for name in LEAF_WIDTHS:
-            exp = sum(a[1][name] for a in all_in)
-            err = max(err, float((grads[name] - exp).abs().max()))
-        ok = (torch.equal(union, exp_union)
-              and err < 1e-5
-              and torch.equal(gmax, torch.stack([a[2] for a in all_in]).max(0).values)
-              and torch.equal(rmax, torch.stack([a[3] for a in all_in]).max(0).values)
-              and torch.equal(denom, sum(a[4] for a in all_in)))
+        ex = ViewDPExchange(bucket_bytes=bucket_bytes, compact_below=compact_below, debug=True)
+        accum, denom, max_radii = initial_state()
+        e_accum, e_denom, e_radii = initial_state()
+        ok, err, info = True, 0.0, None
+        for step in range(STEPS):
+            visible, grads, norm, radii = rank_inputs(rank, step)
+            if use_arena:
+                arena = GradArena(N)
+                for k, v in grads.items():
+                    arena[k].copy_(v)
+                res = ex.exchange(arena, visible, max_stats=[norm, radii])
+                reduced = {k: arena[k] for k in LEAF_WIDTHS}
+            else:
+                res = ex.exchange(grads, visible, max_stats=[norm, radii])
+                reduced = grads
+            # replicated-state update, as the train loop applies it after the exchange
+            accum = torch.maximum(accum, norm)
+            denom += res.view_count
+            max_radii = torch.maximum(max_radii, radii)
+            # expected: the world's views applied one after another (reference semantics)
+            all_in = [rank_inputs(r, step) for r in range(world)]
+            exp_union = torch.zeros(N, dtype=torch.bool)
+            for v, g, nv, rv in all_in:
+                exp_union |= v
+                e_accum[v] = torch.maximum(nv[v], e_accum[v])
+                e_denom[v] += 1
+                e_radii[v] = torch.maximum(e_radii[v], rv[v])
+            for name in LEAF_WIDTHS:
+                exp = sum(a[1][name] for a in all_in)
+                err = max(err, float((reduced[name] - exp).abs().max()))
+            ok = ok and torch.equal(res.union, exp_union) and torch.equal(accum, e_accum) \
+                and torch.equal(denom, e_denom) and torch.equal(max_radii, e_radii)
+            info = (ex.last.union_rows, ex.last.collectives, ex.last.compacted, int(exp_union.sum()))
         if rank == 0:
-            q.put((ok, err, ex.last.union_rows, ex.last.collectives, int(exp_union.sum())))
+            q.put((ok and err < 1e-5, err, info))
     finally:
         dist.destroy_process_group()
 
 
-def run(world, compact, bucket_bytes):
+def run(world, compact_below, bucket_bytes, use_arena):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, world, port, compact, bucket_bytes, q)) for r in range(world)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, compact_below, bucket_bytes, use_arena, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -81,14 +105,21 @@ def run(world, compact, bucket_bytes):
     return q.get(timeout=10)
 
 
-@pytest.mark.parametrize("world,compact,bucket_bytes", [(2, True, 64 << 20), (2, False, 64 << 20),
-                                                        (2, True, 4096), (3, True, 1000)])
-def test_exchange_matches_local_reduction(world, compact, bucket_bytes):
-    ok, err, union_rows, collectives, exp_rows = run(world, compact, bucket_bytes)
+@pytest.mark.parametrize("world,compact_below,bucket_bytes,use_arena", [
+    (2, 1.0, 64 << 20, True),    # compacted (union < 100% of rows)
+    (2, 0.0, 64 << 20, True),    # dense, in place on the arena
+    (2, 0.0, 64 << 20, False),   # dense, separate tensors
+    (2, 1.0, 4096, False),       # compacted, many buckets
+    (3, 1.0, 1000, True),
+])
+def test_multistep_exchange_matches_sequential_reference(world, compact_below, bucket_bytes, use_arena):
+    ok, err, (union_rows, collectives, compacted, exp_rows) = run(world, compact_below, bucket_bytes, use_arena)
     assert ok, f"max grad error {err}"
-    assert union_rows == (exp_rows if compact else N)
-    if bucket_bytes < 4 * 59 * N:  # small buckets -> more than one SUM collective
-        assert collectives > 1 + 2 + 1 + 1
+    assert union_rows == exp_rows
+    assert compacted == (compact_below == 1.0)
+    # one all-gather (masks) + SUM buckets + ONE fused MAX
+    nbytes = 4 * 59 * (exp_rows if compacted else N)
+    assert collectives == 1 + -(-nbytes // bucket_bytes) + 1
 
 
 def test_pack_roundtrip():
@@ -104,6 +135,17 @@ def test_view_index_partition():
     assert sorted(seen) == list(range(5 * world))
 
 
+def test_arena_views_are_param_grads():
+    arena = GradArena(10)
+    p = torch.nn.Parameter(torch.zeros(10, 15, 3))
+    q = torch.nn.Parameter(torch.zeros(10, 3))
+    arena.attach({"f_rest": p, "xyz": q})
+    (p.sum() * 2 + q.sum()).backward()
+    assert p.grad.data_ptr() == arena["f_rest"].data_ptr()
+    assert float(arena["f_rest"].sum()) == 2 * 450 and float(arena["xyz"].sum()) == 30
+    assert arena.flat.numel() == 10 * 59
+
+
 def test_exchange_rejects_bad_inputs():
     ex = ViewDPExchange()
     with pytest.raises(ValueError):
@@ -112,5 +154,20 @@ def test_exchange_rejects_bad_inputs():
         ex.sum_gradients([torch.zeros(3, 2, dtype=torch.float64)])
     with pytest.raises(ValueError):
         ex.sum_gradients([torch.zeros(2, 3).t()])
+    with pytest.raises(ValueError, match="union must be a bool mask"):
+        ex.sum_gradients([torch.zeros(4, 2)], union=torch.ones(3, dtype=torch.bool))
+    with pytest.raises(ValueError, match="union must be a bool mask"):
+        ex.sum_gradients([torch.zeros(4, 2)], union=torch.ones(4))
     with pytest.raises(ValueError):
         ViewDPExchange(bucket_bytes=2)
+    with pytest.raises(ValueError):
+        ViewDPExchange(compact_below=1.5)
+
+
+def test_debug_mode_catches_rows_outside_union():
+    ex = ViewDPExchange(debug=True, compact_below=1.0)
+    g = torch.zeros(6, 2)
+    g[5] = 1.0
+    union = torch.tensor([True, True, False, False, False, False])
+    with pytest.raises(RuntimeError, match="outside the visibility union"):
+        ex.sum_gradients([g], union=union)
