@@ -37,7 +37,7 @@ N_GAUSSIANS = 2_000_000
 W_PX, H_PX = 1920, 1080
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 ROOT = os.path.dirname(os.path.abspath(__file__))
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "latest_kernels.json")  # tools/prof_summary.py output
 
 
 def free_port() -> int:
@@ -143,7 +143,8 @@ def main() -> None:
     traffic = None
     if os.path.exists(TRAFFIC_FILE):
         with open(TRAFFIC_FILE) as f:
-            traffic = json.load(f).get("radix_scatter_u64", {}).get("hbm_bytes_per_launch")
+            nt = (K + 4095) // 4096
+            traffic = json.load(f).get(f"radix_scatter_kernel@{nt * 256}", {}).get("hbm_bytes_per_launch")
     sort_us = sum(kern[k]["avg_us"] * kern[k]["launches_per_step"]
                   for k in ("radix_hist_u64", "radix_digit_scan", "radix_scatter_u64"))
 

@@ -32,6 +32,8 @@
 #include <float.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -247,8 +249,10 @@ __global__ __launch_bounds__(kBlock) void super_box_kernel(const Box* __restrict
 
 // ---- 5. phase 1: one wave per leaf ------------------------------------------------------------
 struct KnnCounters {
-    uint32_t hard;  // number of queries sent to phase 2
-    uint32_t pad[3];
+    uint32_t hard;             // number of queries sent to phase 2
+    uint32_t pad;
+    unsigned long long coarse;  // phase 1: candidate leaves passing the wave-level test
+    unsigned long long fine;    // phase 1: candidate leaves staged and evaluated
 };
 
 __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restrict__ sp, int P, int nleaves, int nsuper,
@@ -309,6 +313,7 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
         const float4 qhi = make_float4(wave_max(active ? p.x : -FLT_MAX), wave_max(active ? p.y : -FLT_MAX),
                                        wave_max(active ? p.z : -FLT_MAX), 0.f);
         float ub = wave_max(active ? b2 : -FLT_MAX);
+        uint32_t n_coarse = 0, n_fine = 0;
         for (int s0 = 0; s0 < nsuper; s0 += kWave) {
             const int s = s0 + lane;
             bool pass = false;
@@ -331,7 +336,9 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
                     const int C = S * kFan + __builtin_ctzll(lmask);
                     lmask &= lmask - 1;
                     const Box cb = leaves[C];
+                    n_coarse++;
                     if (!__ballot(active && box_point_lb(cb, p) <= b2)) continue;
+                    n_fine++;
                     const int cbase = C * kLeaf;
                     const int nc = min(kLeaf, P - cbase);
                     stage[lane] = (lane < nc) ? sp[cbase + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -341,6 +348,10 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
                     ub = wave_max(active ? b2 : -FLT_MAX);
                 }
             }
+        }
+        if (lane == 0) {
+            atomicAdd(&counters->coarse, (unsigned long long)n_coarse);
+            atomicAdd(&counters->fine, (unsigned long long)n_fine);
         }
     }
     if (active) out[__float_as_uint(p.w)] = ((b0 + b1) + b2) / 3.0f;
@@ -490,6 +501,13 @@ int dist_cuda2(hidegs_alloc_fn alloc, void* user, int P, const float* points, fl
                        nsuper, l.leaves, l.supers, mean_dists, l.hard, l.counters);
     HIDEGS_LAUNCH("knn_hard", knn_hard_kernel, dim3(std::min(2048, ceil_div(nleaves, kWaves))), dim3(kBlock), 0, stream, l.sp,
                        P, nleaves, nsuper, l.leaves, l.supers, mean_dists, l.hard, l.counters);
+    if (const char* e = getenv("HIDEGS_KNN_STATS"); e && *e == '1') {
+        KnnCounters h{};
+        if (hipMemcpyAsync(&h, l.counters, sizeof(h), hipMemcpyDeviceToHost, stream) == hipSuccess &&
+            hipStreamSynchronize(stream) == hipSuccess)
+            fprintf(stderr, "[hidegs knn] P=%d leaves=%d supers=%d hard=%u coarse_leaves/wave=%.2f fine_leaves/wave=%.2f\n",
+                    P, nleaves, nsuper, h.hard, (double)h.coarse / nleaves, (double)h.fine / nleaves);
+    }
     return check_launch("distCUDA2", stream, 0);
 }
 
