@@ -126,27 +126,36 @@ def main() -> None:
 
     # per-kernel durations of the same step, live, with per-launch HIP events
     kt_steps = max(10, min(args.steps, 50))
+    # algorithmic bytes per launch (SURVEY §8(d) D4 per-pair figures: a sort pass reads and writes
+    # key 8 + value 4; a histogram or range pass reads the 8-byte keys; the scan reads and writes u32)
+    alg = {"scan_reduce": 4 * N_GAUSSIANS, "scan_small": 0, "scan_downsweep": 8 * N_GAUSSIANS,
+           "radix_hist_u64": 8 * K, "radix_digit_scan": 0, "radix_scatter_u64": 24 * K,
+           "segment_ranges": 8 * K, "segment_sort": 24 * K, "segment_sort_big": 0, "identify_ranges": 8 * K}
     with _lib.kernel_timer() as kt:
         for _ in range(kt_steps):
             step()
         torch.cuda.synchronize()
-        names = ["scan_reduce", "scan_small", "scan_downsweep", "radix_hist_u64", "radix_digit_scan",
-                 "radix_scatter_u64", "identify_ranges"]
         kern = {}
-        for nm in names:
+        for nm, nbytes in alg.items():
             ms, n = kt.get(nm)
-            kern[nm] = {"avg_us": round(ms * 1e3 / max(n, 1), 2), "launches_per_step": n // kt_steps}
-    passes = kern["radix_scatter_u64"]["launches_per_step"]
-    scat_us = kern["radix_scatter_u64"]["avg_us"]
-    scat_bytes = 24 * K                            # per launch: read key+value, write key+value
-    achieved = scat_bytes / (scat_us * 1e-6) / 1e9
+            if n == 0:
+                continue
+            avg_us = ms * 1e3 / n
+            kern[nm] = {"avg_us": round(avg_us, 2), "launches_per_step": n // kt_steps,
+                        "us_per_step": round(ms * 1e3 / kt_steps, 2),
+                        "GBps": round(nbytes / (avg_us * 1e-6) / 1e9, 1) if nbytes else None}
+    dom = max((k for k in kern if alg[k]), key=lambda k: kern[k]["us_per_step"])
+    dom_us = kern[dom]["avg_us"]
+    dom_bytes = alg[dom]
+    achieved = dom_bytes / (dom_us * 1e-6) / 1e9
     traffic = None
+    rocprof_name = {"radix_scatter_u64": "radix_scatter_kernel", "segment_sort": "segment_sort_kernel",
+                    "radix_hist_u64": "radix_hist_kernel"}.get(dom, dom + "_kernel")
+    grid = {"segment_sort": T * 256}.get(dom, ((K + 4095) // 4096) * 256)
     if os.path.exists(TRAFFIC_FILE):
         with open(TRAFFIC_FILE) as f:
-            nt = (K + 4095) // 4096
-            traffic = json.load(f).get(f"radix_scatter_kernel@{nt * 256}", {}).get("hbm_bytes_per_launch")
-    sort_us = sum(kern[k]["avg_us"] * kern[k]["launches_per_step"]
-                  for k in ("radix_hist_u64", "radix_digit_scan", "radix_scatter_u64"))
+            traffic = json.load(f).get(f"{rocprof_name}@{grid}", {}).get("hbm_bytes_per_launch")
+    sort_us = sum(kern[k]["us_per_step"] for k in kern if k.startswith(("radix_", "segment_")))
 
     line = {
         "metric": "fwd+bwd iters/sec & HBM GB/s at 2M Gaussians, 1920x1080",
@@ -170,11 +179,10 @@ def main() -> None:
         "binning_step": {"ms_per_step": round(ms_step, 4), "wall_ms_per_step": round(wall_ms_step, 4),
                          "pairs_per_s_all_ranks": K * world / (ms_step * 1e-3),
                          "views_per_s_all_ranks": world / (ms_step * 1e-3),
-                         "sort_passes": passes, "sort_us": round(sort_us, 2), "kernels": kern},
-        "roofline": {"kernel": "radix_scatter_u64", "bound": "hbm", "achieved": round(achieved, 1),
+                         "sort_us": round(sort_us, 2), "kernels": kern},
+        "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic, "algorithmic_bytes_per_launch": scat_bytes,
-                     "avg_launch_us": scat_us},
+                     "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": dom_us},
         "cpu_baseline": None,
     }
 

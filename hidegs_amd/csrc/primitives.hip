@@ -174,6 +174,52 @@ __device__ __forceinline__ uint32_t digit_of(K key, int shift, uint32_t mask)
     return (uint32_t)(key >> shift) & mask;
 }
 
+// Stable wave64 ranking of R rounds of items (round r, lane l = the wave's item r*64 + l,
+// in input order).  cnt = this wave's 256 digit counters, zero on entry; on exit cnt[d] is
+// the number of valid items with digit d and rank[r] the item's position among them.
+// The lanes sharing a digit are found with kRadixBits ballots; the lowest such lane bumps
+// the counter (LDS ops of one wave retire in order, so the read precedes the write).
+template <typename K, int R>
+__device__ __forceinline__ void wave_rank(const K (&k)[R], const bool (&ok)[R], int shift, uint32_t mask,
+                                          uint32_t* cnt, uint32_t (&rank)[R])
+{
+    const int lane = lane_id();
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint32_t d = digit_of(k[r], shift, mask);
+        uint64_t m = __ballot(ok[r]);
+#pragma unroll
+        for (int b = 0; b < kRadixBits; b++) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const uint32_t below = (uint32_t)__popcll(m & lt);
+        uint32_t old = 0;
+        if (ok[r]) old = cnt[d];
+        __builtin_amdgcn_wave_barrier();
+        if (ok[r] && below == 0) cnt[d] = old + (uint32_t)__popcll(m);
+        __builtin_amdgcn_wave_barrier();
+        rank[r] = old + below;
+    }
+}
+
+// After every wave ranked (and a __syncthreads): thread d turns s_cnt[w][d] into the count of
+// digit d in waves < w and returns the block's total for digit d.
+__device__ __forceinline__ uint32_t digit_wave_prefix(uint32_t (*s_cnt)[kRadix])
+{
+    const int d = threadIdx.x;  // kBlock == kRadix
+    uint32_t run = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; w++) {
+        const uint32_t c = s_cnt[w][d];
+        s_cnt[w][d] = run;
+        run += c;
+    }
+    return run;
+}
+
 // counts[d * ntiles + tile] = number of keys of tile `tile` whose digit is d.
 template <typename K>
 __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const K* __restrict__ keys, long long n, int shift,
@@ -235,6 +281,9 @@ __global__ __launch_bounds__(kBlock) void radix_digit_scan_kernel(uint32_t* __re
 }
 
 // Stable scatter of one tile.  LDS: keys + values of the tile, per-wave digit counters.
+// Global offsets: tile_prefix[d][tile] (per-digit exclusive scan over tiles) + exclusive scan
+// of the digit totals.  (A single-pass decoupled look-back variant measured slower on MI355X:
+// the chained tile-to-tile hand-off crosses the non-coherent per-XCD L2s at every hop.)
 template <typename K>
 __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restrict__ keys_in,
                                                                const uint32_t* __restrict__ vals_in,
@@ -252,94 +301,270 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
     const int t = threadIdx.x;
     const int lane = lane_id();
     const int wave = t / kWave;
+    for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
     const long long base = (long long)blockIdx.x * kTile;
     const long long seg = base + (long long)wave * (kItems * kWave);  // this wave's 1024 items
 
-    for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
-
     K k[kItems];
     uint32_t v[kItems];
+    bool ok[kItems];
 #pragma unroll
     for (int r = 0; r < kItems; r++) {
-        long long i = seg + r * kWave + lane;
-        bool ok = i < n;
-        k[r] = ok ? keys_in[i] : K(0);
-        v[r] = ok ? vals_in[i] : 0u;
+        const long long i = seg + r * kWave + lane;
+        ok[r] = i < n;
+        k[r] = ok[r] ? keys_in[i] : K(0);
+        v[r] = ok[r] ? vals_in[i] : 0u;
     }
     __syncthreads();
-
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t rank[kItems];
-#pragma unroll
-    for (int r = 0; r < kItems; r++) {
-        long long i = seg + r * kWave + lane;
-        const bool ok = i < n;
-        const uint32_t d = digit_of(k[r], shift, mask);
-        uint64_t m = __ballot(ok);
-#pragma unroll
-        for (int b = 0; b < kRadixBits; b++) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            m &= bit ? bb : ~bb;
-        }
-        const uint32_t below = (uint32_t)__popcll(m & lt);
-        const uint32_t cnt = (uint32_t)__popcll(m);
-        uint32_t old = 0;
-        if (ok) old = s_cnt[wave][d];
-        __builtin_amdgcn_wave_barrier();
-        if (ok && below == 0) s_cnt[wave][d] = old + cnt;
-        __builtin_amdgcn_wave_barrier();
-        rank[r] = old + below;
-    }
+    wave_rank<K, kItems>(k, ok, shift, mask, s_cnt[wave], rank);
     __syncthreads();
 
-    // digit d: prefix over waves, tile total, then tile-local run starts
-    uint32_t tile_count_d = 0;
-    {
-        const int d = t;  // kBlock == kRadix
-        uint32_t run = 0;
-#pragma unroll
-        for (int w = 0; w < kWavesPerBlock; w++) {
-            uint32_t c = s_cnt[w][d];
-            s_cnt[w][d] = run;
-            run += c;
-        }
-        tile_count_d = run;
-    }
+    const int d = t;
+    const uint32_t tile_count_d = digit_wave_prefix(s_cnt);
     uint32_t dummy;
-    const uint32_t start_d = block_exclusive_scan(tile_count_d, s_wave, &dummy);
-    s_start[t] = start_d;
+    s_start[d] = block_exclusive_scan(tile_count_d, s_wave, &dummy);
     __syncthreads();
-
 #pragma unroll
     for (int r = 0; r < kItems; r++) {
-        long long i = seg + r * kWave + lane;
-        if (i < n) {
-            const uint32_t d = digit_of(k[r], shift, mask);
-            const uint32_t pos = s_start[d] + s_cnt[wave][d] + rank[r];
+        if (ok[r]) {
+            const uint32_t dd = digit_of(k[r], shift, mask);
+            const uint32_t pos = s_start[dd] + s_cnt[wave][dd] + rank[r];
             s_keys[pos] = k[r];
             s_vals[pos] = v[r];
         }
     }
     __syncthreads();
-
-    // global offset of digit d for this tile = sum of totals of smaller digits + tile prefix
     {
-        const int d = t;
-        uint32_t tot = totals[d];
-        uint32_t dbase = block_exclusive_scan(tot, s_wave, &dummy);
+        const uint32_t dbase = block_exclusive_scan(totals[d], s_wave, &dummy);
         s_cnt[0][d] = dbase + tile_prefix[(long long)d * ntiles + blockIdx.x] - s_start[d];
     }
     __syncthreads();
-
     const int count = (int)((n - base) < kTile ? (n - base) : kTile);
     for (int i = t; i < count; i += kBlock) {
         const K key = s_keys[i];
-        const uint32_t d = digit_of(key, shift, mask);
-        const uint32_t dst = s_cnt[0][d] + i;
+        const uint32_t dst = s_cnt[0][digit_of(key, shift, mask)] + i;
         if (dst < n) {  // always true for consistent counts; never write outside the output
             keys_out[dst] = key;
             vals_out[dst] = s_vals[i];
+        }
+    }
+}
+
+// ============================== segmented sort =================================
+//
+// Keys whose bits [32, end_bit) are a small segment id -- the (tile | depth) keys of the
+// binning stage -- are sorted in two stages with the same result as the LSD sort over
+// [0, end_bit): (1) the LSD passes above over [32, end_bit) only, which partition the pairs
+// stably by segment; (2) one workgroup per segment sorts it stably by the low 32 bits in LDS
+// (passes whose digit is constant over the segment are skipped).  Segments larger than
+// kSegCap go to a list that a second kernel sorts with one workgroup each, through global
+// memory, 4096 items at a time.  Global traffic drops from 6 LSD passes to 2 plus one
+// read/write of every pair.
+
+constexpr int kSegCap = 2048;
+constexpr int kSegRounds = kSegCap / kBlock;  // rounds of 64 per wave
+
+__global__ __launch_bounds__(kBlock) void segment_sort_kernel(uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                              const uint2* __restrict__ ranges,
+                                                              uint32_t* __restrict__ overflow,
+                                                              uint32_t* __restrict__ n_overflow)
+{
+    // LDS holds (low 32 key bits, original index) pairs; the full keys and values stay in
+    // registers and are exchanged through LDS once, by original index, after the last pass.
+    __shared__ __attribute__((aligned(16))) uint32_t s_k[2][kSegCap];
+    __shared__ __attribute__((aligned(16))) uint32_t s_i[2][kSegCap];
+    __shared__ uint32_t s_cnt[kWavesPerBlock][kRadix];
+    __shared__ uint32_t s_start[kRadix];
+    __shared__ uint32_t s_wave[kWavesPerBlock];
+    __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock];
+
+    const int t = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = t / kWave;
+    const uint2 r = ranges[blockIdx.x];
+    const uint32_t begin = r.x, m = r.y - r.x;
+    if (r.y <= r.x + 1) return;  // absent or single pair: already in place
+    if (m > (uint32_t)kSegCap) {
+        if (t == 0) overflow[atomicAdd(n_overflow, 1u)] = blockIdx.x;
+        return;
+    }
+    // all loads issued before any is used: item t + 256 q
+    uint64_t kin[kSegRounds];
+    uint32_t vin[kSegRounds];
+#pragma unroll
+    for (int q = 0; q < kSegRounds; q++) {
+        const uint32_t i = t + q * kBlock;
+        kin[q] = i < m ? keys[begin + i] : 0ull;
+        vin[q] = i < m ? vals[begin + i] : 0u;
+    }
+    uint32_t a = 0xffffffffu, o = 0;
+#pragma unroll
+    for (int q = 0; q < kSegRounds; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            s_k[0][i] = (uint32_t)kin[q];
+            s_i[0][i] = i;
+            a &= (uint32_t)kin[q];
+            o |= (uint32_t)kin[q];
+        }
+    }
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        a &= __shfl_xor(a, sh, kWave);
+        o |= __shfl_xor(o, sh, kWave);
+    }
+    if (lane == 0) {
+        s_and[wave] = a;
+        s_or[wave] = o;
+    }
+    __syncthreads();
+    uint32_t diff;
+    {
+        uint32_t aa = 0xffffffffu, oo = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; w++) {
+            aa &= s_and[w];
+            oo |= s_or[w];
+        }
+        diff = aa ^ oo;  // bits that vary over the segment
+    }
+    // wave w ranks items [w*C, w*C + C) in (round, lane) order; C is a multiple of 64
+    const uint32_t C = ((m + kBlock - 1) / kBlock) * kWave;
+    const int rounds = (int)(C / kWave);
+    const uint32_t w0 = wave * C;
+    int cur = 0;
+    for (int shift = 0; shift < 32; shift += kRadixBits) {
+        if (((diff >> shift) & (kRadix - 1)) == 0) continue;  // digit constant over the segment
+        for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t k[kSegRounds], id[kSegRounds], rank[kSegRounds];
+        bool ok[kSegRounds];
+#pragma unroll
+        for (int q = 0; q < kSegRounds; q++) {
+            const uint32_t i = w0 + q * kWave + lane;
+            ok[q] = q < rounds && i < m;
+            k[q] = ok[q] ? s_k[cur][i] : 0u;
+            id[q] = ok[q] ? s_i[cur][i] : 0u;
+        }
+        // the ranking of rounds >= `rounds` is skipped as a whole (block-uniform)
+        if (rounds == kSegRounds) {
+            wave_rank<uint32_t, kSegRounds>(k, ok, shift, kRadix - 1, s_cnt[wave], rank);
+        } else {
+#pragma unroll
+            for (int q = 0; q < kSegRounds; q++) {
+                if (q < rounds) {
+                    uint32_t kk[1] = {k[q]}, rr[1];
+                    bool oo[1] = {ok[q]};
+                    wave_rank<uint32_t, 1>(kk, oo, shift, kRadix - 1, s_cnt[wave], rr);
+                    rank[q] = rr[0];
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t tot = digit_wave_prefix(s_cnt);
+        uint32_t dummy;
+        s_start[t] = block_exclusive_scan(tot, s_wave, &dummy);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kSegRounds; q++) {
+            if (ok[q]) {
+                const uint32_t dd = digit_of(k[q], shift, kRadix - 1);
+                const uint32_t pos = s_start[dd] + s_cnt[wave][dd] + rank[q];
+                s_k[cur ^ 1][pos] = k[q];
+                s_i[cur ^ 1][pos] = id[q];
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    // exchange full keys (high half) and values by original index through the free buffer
+#pragma unroll
+    for (int q = 0; q < kSegRounds; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            s_k[cur ^ 1][i] = (uint32_t)(kin[q] >> 32);
+            s_i[cur ^ 1][i] = vin[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kSegRounds; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            const uint32_t src = s_i[cur][i];
+            keys[begin + i] = ((uint64_t)s_k[cur ^ 1][src] << 32) | s_k[cur][i];
+            vals[begin + i] = s_i[cur ^ 1][src];
+        }
+    }
+}
+
+// One workgroup per oversized segment: 4 stable LSD passes over the low 32 bits through
+// global memory (keys/vals <-> alt within the segment's range), 4096 items per step.
+__global__ __launch_bounds__(kBlock) void segment_sort_big_kernel(uint64_t* __restrict__ keys,
+                                                                  uint32_t* __restrict__ vals,
+                                                                  uint64_t* __restrict__ alt_k,
+                                                                  uint32_t* __restrict__ alt_v,
+                                                                  const uint2* __restrict__ ranges,
+                                                                  const uint32_t* __restrict__ overflow,
+                                                                  const uint32_t* __restrict__ n_overflow)
+{
+    __shared__ uint32_t s_cnt[kWavesPerBlock][kRadix];
+    __shared__ uint32_t s_hist[kRadix];
+    __shared__ uint32_t s_run[kRadix];  // running global start of each digit within the segment
+    __shared__ uint32_t s_wave[kWavesPerBlock];
+    const int t = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = t / kWave;
+    const uint32_t nover = *n_overflow;
+    for (uint32_t o = blockIdx.x; o < nover; o += gridDim.x) {
+        const uint2 r = ranges[overflow[o]];
+        const uint32_t begin = r.x, m = r.y - r.x;
+        for (int pass = 0; pass < 4; pass++) {
+            const int shift = pass * kRadixBits;
+            const uint64_t* sk = (pass & 1) ? alt_k : keys;
+            const uint32_t* sv = (pass & 1) ? alt_v : vals;
+            uint64_t* dk = (pass & 1) ? keys : alt_k;
+            uint32_t* dv = (pass & 1) ? vals : alt_v;
+            s_hist[t] = 0;
+            __syncthreads();
+            for (uint32_t i = t; i < m; i += kBlock) atomicAdd(&s_hist[digit_of(sk[begin + i], shift, kRadix - 1)], 1u);
+            __syncthreads();
+            uint32_t dummy;
+            s_run[t] = begin + block_exclusive_scan(s_hist[t], s_wave, &dummy);
+            __syncthreads();
+            for (uint32_t c0 = 0; c0 < m; c0 += kTile) {
+                for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
+                __syncthreads();
+                uint64_t k[kItems];
+                uint32_t v[kItems];
+                bool ok[kItems];
+                uint32_t rank[kItems];
+                const uint32_t w0 = c0 + wave * (kItems * kWave);
+#pragma unroll
+                for (int q = 0; q < kItems; q++) {
+                    const uint32_t i = w0 + q * kWave + lane;
+                    ok[q] = i < m;
+                    k[q] = ok[q] ? sk[begin + i] : 0ull;
+                    v[q] = ok[q] ? sv[begin + i] : 0u;
+                }
+                wave_rank<uint64_t, kItems>(k, ok, shift, kRadix - 1, s_cnt[wave], rank);
+                __syncthreads();
+                const uint32_t tot = digit_wave_prefix(s_cnt);
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < kItems; q++) {
+                    if (ok[q]) {
+                        const uint32_t dd = digit_of(k[q], shift, kRadix - 1);
+                        const uint32_t dst = s_run[dd] + s_cnt[wave][dd] + rank[q];
+                        dk[dst] = k[q];
+                        dv[dst] = v[q];
+                    }
+                }
+                __syncthreads();
+                s_run[t] += tot;
+                __syncthreads();
+            }
         }
     }
 }
@@ -348,16 +573,19 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
 
 // Tile ids >= num_tiles violate the caller contract; their entries are skipped rather
 // than written out of bounds.
+// tile = (key >> 32) & tile_mask (the public entry point passes all ones; the segmented sort
+// masks to its segment bits).
 __global__ __launch_bounds__(kBlock) void identify_ranges_kernel(const uint64_t* __restrict__ keys, long long n,
-                                                                 uint2* __restrict__ ranges, uint32_t num_tiles)
+                                                                 uint2* __restrict__ ranges, uint32_t num_tiles,
+                                                                 uint32_t tile_mask)
 {
     const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    const uint32_t cur = (uint32_t)(keys[i] >> 32);
+    const uint32_t cur = (uint32_t)(keys[i] >> 32) & tile_mask;
     if (i == 0) {
         if (cur < num_tiles) ranges[cur].x = 0;
     } else {
-        const uint32_t prev = (uint32_t)(keys[i - 1] >> 32);
+        const uint32_t prev = (uint32_t)(keys[i - 1] >> 32) & tile_mask;
         if (cur != prev) {
             if (prev < num_tiles) ranges[prev].y = (uint32_t)i;
             if (cur < num_tiles) ranges[cur].x = (uint32_t)i;
@@ -374,13 +602,23 @@ size_t scan_scratch(long long n)
     return align_up((size_t)nt * sizeof(uint32_t)) + align_up(sizeof(uint32_t));
 }
 
+constexpr int kMaxSegmentBits = 16;        // segmented path: at most 65536 segments
+constexpr long long kSegmentedMinN = 65536;  // below this the plain LSD passes are cheaper
+
 template <typename K>
 size_t sort_scratch(long long n)
 {
     const int nt = ceil_div(n, kTile);
-    return align_up((size_t)n * sizeof(K)) + align_up((size_t)n * sizeof(uint32_t)) +
-           align_up((size_t)kRadix * nt * sizeof(uint32_t)) + align_up(kRadix * sizeof(uint32_t));
+    size_t b = align_up((size_t)n * sizeof(K)) + align_up((size_t)n * sizeof(uint32_t)) +
+               align_up((size_t)kRadix * nt * sizeof(uint32_t)) + align_up(kRadix * sizeof(uint32_t));
+    if (sizeof(K) == 8)  // segmented path: ranges, overflow list and its counter
+        b += align_up(sizeof(uint2) << kMaxSegmentBits) + align_up(sizeof(uint32_t) << kMaxSegmentBits) +
+             align_up(sizeof(uint32_t));
+    return b;
 }
+
+__global__ void identify_ranges_kernel(const uint64_t* __restrict__ keys, long long n, uint2* __restrict__ ranges,
+                                       uint32_t num_tiles, uint32_t tile_mask);
 
 template <typename K>
 int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
@@ -412,21 +650,45 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
     uint32_t* counts = c.take<uint32_t>((size_t)kRadix * nt);
     uint32_t* totals = c.take<uint32_t>(kRadix);
 
+    // (tile | depth)-shaped sort: LSD over the segment bits only, then per-segment LDS sorts
+    const bool segmented = sizeof(K) == 8 && begin_bit == 0 && end_bit > 32 && end_bit - 32 <= kMaxSegmentBits &&
+                           n >= kSegmentedMinN;
+    const int lo_bit = segmented ? 32 : begin_bit;
+    const int lsd_passes = segmented ? (end_bit - 32 + kRadixBits - 1) / kRadixBits : passes;
+
     const K* src_k = keys_in;
     const uint32_t* src_v = vals_in;
-    for (int p = 0; p < passes; p++) {
-        const int shift = begin_bit + p * kRadixBits;
+    for (int p = 0; p < lsd_passes; p++) {
+        const int shift = lo_bit + p * kRadixBits;
         const int bits = (end_bit - shift) < kRadixBits ? (end_bit - shift) : kRadixBits;
         const uint32_t mask = (1u << bits) - 1u;
-        const bool to_out = ((passes - 1 - p) % 2) == 0;
+        const bool to_out = ((lsd_passes - 1 - p) % 2) == 0;
         K* dk = to_out ? keys_out : alt_k;
         uint32_t* dv = to_out ? vals_out : alt_v;
-        HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_hist_u64" : "radix_hist_u32"), radix_hist_kernel<K>, dim3(nt), dim3(kBlock), 0, stream, src_k, n, shift, mask, nt, counts);
-        HIDEGS_LAUNCH("radix_digit_scan", radix_digit_scan_kernel, dim3(kRadix), dim3(kBlock), 0, stream, counts, nt, totals);
-        HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"), radix_scatter_kernel<K>, dim3(nt), dim3(kBlock), 0, stream, src_k, src_v, dk, dv, n, shift,
-                           mask, nt, counts, totals);
+        HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_hist_u64" : "radix_hist_u32"), radix_hist_kernel<K>, dim3(nt),
+                      dim3(kBlock), 0, stream, src_k, n, shift, mask, nt, counts);
+        HIDEGS_LAUNCH("radix_digit_scan", radix_digit_scan_kernel, dim3(kRadix), dim3(kBlock), 0, stream, counts, nt,
+                      totals);
+        HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"), radix_scatter_kernel<K>,
+                      dim3(nt), dim3(kBlock), 0, stream, src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals);
         src_k = dk;
         src_v = dv;
+    }
+    if (segmented) {
+        const int nseg = 1 << (end_bit - 32);
+        uint2* ranges = c.take<uint2>((size_t)1 << kMaxSegmentBits);
+        uint32_t* overflow = c.take<uint32_t>((size_t)1 << kMaxSegmentBits);
+        uint32_t* n_overflow = c.take<uint32_t>(1);
+        uint64_t* ko = reinterpret_cast<uint64_t*>(keys_out);
+        if (hipMemsetAsync(ranges, 0, sizeof(uint2) * nseg, stream) != hipSuccess ||
+            hipMemsetAsync(n_overflow, 0, sizeof(uint32_t), stream) != hipSuccess)
+            return fail(HIDEGS_E_HIP, std::string(what) + ": memset failed");
+        HIDEGS_LAUNCH("segment_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock)), dim3(kBlock), 0, stream,
+                      (const uint64_t*)ko, n, ranges, (uint32_t)nseg, (uint32_t)(nseg - 1));
+        HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out, ranges,
+                      overflow, n_overflow);
+        HIDEGS_LAUNCH("segment_sort_big", segment_sort_big_kernel, dim3(nseg < 512 ? nseg : 512), dim3(kBlock), 0,
+                      stream, ko, vals_out, reinterpret_cast<uint64_t*>(alt_k), alt_v, ranges, overflow, n_overflow);
     }
     return check_launch(what, stream, 0);
 }
@@ -473,7 +735,7 @@ int identify_tile_ranges(const uint64_t* keys, long long n, uint32_t* ranges, in
     if (n == 0) return check_launch("identify_tile_ranges", stream, 0);
     if (!keys) return fail(HIDEGS_E_ARG, "identify_tile_ranges: NULL keys");
     HIDEGS_LAUNCH("identify_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock)), dim3(kBlock), 0, stream, keys, n,
-                       reinterpret_cast<uint2*>(ranges), (uint32_t)num_tiles);
+                       reinterpret_cast<uint2*>(ranges), (uint32_t)num_tiles, 0xffffffffu);
     return check_launch("identify_tile_ranges", stream, 0);
 }
 

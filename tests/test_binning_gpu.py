@@ -36,7 +36,25 @@ def test_sort_raster_keys_bit_exact(K, T):
     assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
 
 
-@pytest.mark.parametrize("begin,end", [(0, 64), (8, 40), (3, 17), (0, 0), (60, 64)])
+@pytest.mark.parametrize("K,T,hot", [(400_000, 64, 0.0), (1_000_000, 8160, 0.3), (2_000_000, 32400, 0.05),
+                                     (70_000, 65536, 0.0)])
+def test_segmented_sort_small_and_oversized_tiles_bit_exact(K, T, hot):
+    """The segmented path: tiles of a few pairs (LDS sort), and hot tiles with far more than the
+    2048-pair LDS capacity (the one-workgroup global fallback); `hot` of the pairs go to 5 tiles."""
+    keys, vals = raster_like_keys(K, T, K + T)
+    g = np.random.default_rng(1)
+    hot_idx = g.random(K) < hot
+    hot_tiles = g.integers(0, T, 5).astype(np.uint64)
+    keys[hot_idx] = (hot_tiles[g.integers(0, 5, int(hot_idx.sum()))] << np.uint64(32)) | (keys[hot_idx] & np.uint64(0xFFFFFFFF))
+    keys[::11] = keys[5]  # equal keys across tiles: stability is observable
+    end = 32 + primitives.higher_msb(T)
+    ko, vo = primitives.sort_pairs(u64(keys), u32(vals), 0, end)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, end)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+
+
+@pytest.mark.parametrize("begin,end", [(0, 64), (8, 40), (3, 17), (0, 0), (60, 64), (0, 40), (0, 48), (0, 33)])
 def test_sort_u64_bit_ranges_and_stability(begin, end):
     g = np.random.default_rng(begin * 100 + end)
     keys = g.integers(0, 2**63, 300_001, dtype=np.uint64) | (g.integers(0, 2, 300_001, dtype=np.uint64) << np.uint64(63))
