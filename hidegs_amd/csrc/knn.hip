@@ -32,6 +32,7 @@
 #include <float.h>
 
 #include <algorithm>
+#include <vector>
 #include <cstdio>
 #include <cstdlib>
 
@@ -49,6 +50,7 @@ constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / kWave;  // 4 waves = 4 leaves per workgroup
 constexpr int kLeaf = 64;               // points per leaf
 constexpr int kFan = 64;                // leaves per super-box
+constexpr int kSub = 4;                 // sub-boxes per leaf (16 points each): the fine filter
 constexpr int kMortonBits = 16;         // per axis
 constexpr int kBoundBlocks = 1024;
 constexpr float kHardFactor = 8.0f;     // 3rd-best above 8x the wave mean -> phase 2
@@ -92,6 +94,47 @@ __device__ __forceinline__ void kbest(float d, float& b0, float& b1, float& b2)
     b2 = fminf(b2, u1);
     b1 = t1;
     b0 = t0;
+}
+
+// Value of lane `src` as a wave-uniform (scalar-register) float.
+__device__ __forceinline__ float uniform_lane(float v, int src)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+
+// Evaluates the kChunk candidates held by lanes k0 .. k0 + kChunk of `c` (one point per lane) against
+// query p: each candidate is broadcast with v_readlane into scalar registers, so the loop has no
+// memory latency at all.  Candidates at or past `nvalid` and the query itself (lane `self`) enter as
+// FLT_MAX, which leaves the three best unchanged exactly as skipping them would.
+__device__ __forceinline__ void eval_lanes(float4 c, int k0, int nvalid, int self, float4 p, float& b0, float& b1,
+                                           float& b2)
+{
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int k = k0 + j;
+        const float4 q = make_float4(uniform_lane(c.x, k), uniform_lane(c.y, k), uniform_lane(c.z, k), 0.f);
+        const float d = sqdist(p, q);
+        kbest((k < nvalid && k != self) ? d : FLT_MAX, b0, b1, b2);
+    }
+}
+
+// Evaluates kChunk staged candidates stage[k0 .. k0 + kChunk) against query p.  All LDS reads and
+// distances are independent and issued first; only the insertion chain is serial.  Candidates at
+// or past `nvalid` and the query itself (index `self`) enter as FLT_MAX, which leaves the three
+// best unchanged exactly as skipping them would.
+constexpr int kChunk = 16;
+__device__ __forceinline__ void eval_chunk(const float4* stage, int k0, int nvalid, int self, float4 p, float& b0,
+                                           float& b1, float& b2)
+{
+#pragma unroll
+    for (int h = 0; h < kChunk; h += kChunk / 2) {
+        float d[kChunk / 2];
+#pragma unroll
+        for (int j = 0; j < kChunk / 2; j++) d[j] = sqdist(p, stage[k0 + h + j]);
+#pragma unroll
+        for (int j = 0; j < kChunk / 2; j++)
+            kbest((k0 + h + j < nvalid && k0 + h + j != self) ? d[j] : FLT_MAX, b0, b1, b2);
+    }
 }
 
 __device__ __forceinline__ int xcd_swizzle(int b, int nb)
@@ -221,16 +264,36 @@ __device__ __forceinline__ Box wave_box(float4 p, bool valid)
     return b;
 }
 
+// Leaf boxes and, per leaf, kSub sub-boxes of kLeaf / kSub consecutive points (the fine filter).
 __global__ __launch_bounds__(kBlock) void leaf_box_kernel(const float4* __restrict__ sp, int P, int nleaves,
-                                                          Box* __restrict__ leaves)
+                                                          Box* __restrict__ leaves, Box* __restrict__ subs)
 {
     const int L = blockIdx.x * kWaves + threadIdx.x / kWave;
     if (L >= nleaves) return;
-    const int i = L * kLeaf + lane_id();
+    const int lane = lane_id();
+    const int i = L * kLeaf + lane;
     const bool valid = i < P;
     const float4 p = valid ? sp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const Box b = wave_box(p, valid);
-    if (lane_id() == 0) leaves[L] = b;
+    float v[6] = {valid ? p.x : FLT_MAX,  valid ? p.y : FLT_MAX,  valid ? p.z : FLT_MAX,
+                  valid ? p.x : -FLT_MAX, valid ? p.y : -FLT_MAX, valid ? p.z : -FLT_MAX};
+    // reduce inside groups of kLeaf / kSub lanes, store the sub-box, then finish across groups
+#pragma unroll
+    for (int m = 1; m < kLeaf / kSub; m <<= 1)
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+            const float o = __shfl_xor(v[a], m, kWave);
+            v[a] = a < 3 ? fminf(v[a], o) : fmaxf(v[a], o);
+        }
+    if ((lane % (kLeaf / kSub)) == 0)
+        subs[L * kSub + lane / (kLeaf / kSub)] = Box{make_float4(v[0], v[1], v[2], 0.f), make_float4(v[3], v[4], v[5], 0.f)};
+#pragma unroll
+    for (int m = kLeaf / kSub; m < kWave; m <<= 1)
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+            const float o = __shfl_xor(v[a], m, kWave);
+            v[a] = a < 3 ? fminf(v[a], o) : fmaxf(v[a], o);
+        }
+    if (lane == 0) leaves[L] = Box{make_float4(v[0], v[1], v[2], 0.f), make_float4(v[3], v[4], v[5], 0.f)};
 }
 
 __global__ __launch_bounds__(kBlock) void super_box_kernel(const Box* __restrict__ leaves, int nleaves, int nsuper,
@@ -248,24 +311,67 @@ __global__ __launch_bounds__(kBlock) void super_box_kernel(const Box* __restrict
 }
 
 // ---- 5. phase 1: one wave per leaf ------------------------------------------------------------
+constexpr int kGroups = 4;                  // query groups per wave for the coarse filter
+constexpr int kSuperBatch = 4;              // super-boxes tested per lane per batch
+constexpr int kLeafBatch = 4;               // passing super-boxes whose leaf boxes load together
+constexpr int kListCap = 256;               // candidate leaves buffered per wave
+constexpr int kFlushBatch = 4;              // candidate leaves loaded together
+constexpr int kGroupLanes = kWave / kGroups;
+
+// Boxes of the active queries of each group of kGroupLanes lanes, broadcast to every lane.
+__device__ __forceinline__ void group_boxes(float4 p, bool active, float4 (&lo)[kGroups], float4 (&hi)[kGroups])
+{
+    float v[6] = {active ? p.x : FLT_MAX,  active ? p.y : FLT_MAX,  active ? p.z : FLT_MAX,
+                  active ? p.x : -FLT_MAX, active ? p.y : -FLT_MAX, active ? p.z : -FLT_MAX};
+#pragma unroll
+    for (int m = 1; m < kGroupLanes; m <<= 1)
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+            const float o = __shfl_xor(v[a], m, kWave);
+            v[a] = a < 3 ? fminf(v[a], o) : fmaxf(v[a], o);
+        }
+#pragma unroll
+    for (int g = 0; g < kGroups; g++) {
+        lo[g] = make_float4(uniform_lane(v[0], g * kGroupLanes), uniform_lane(v[1], g * kGroupLanes),
+                            uniform_lane(v[2], g * kGroupLanes), 0.f);
+        hi[g] = make_float4(uniform_lane(v[3], g * kGroupLanes), uniform_lane(v[4], g * kGroupLanes),
+                            uniform_lane(v[5], g * kGroupLanes), 0.f);
+    }
+}
+
+// Upper bound of the 3rd-best distance over each group's active queries (-FLT_MAX if none).
+__device__ __forceinline__ void group_bounds(float b2, bool active, float (&ub)[kGroups])
+{
+    float v = active ? b2 : -FLT_MAX;
+#pragma unroll
+    for (int m = 1; m < kGroupLanes; m <<= 1) v = fmaxf(v, __shfl_xor(v, m, kWave));
+#pragma unroll
+    for (int g = 0; g < kGroups; g++) ub[g] = uniform_lane(v, g * kGroupLanes);
+}
+
+// ---- phase 1 kernel ------------------------------------------------------------
 struct KnnCounters {
     uint32_t hard;             // number of queries sent to phase 2
     uint32_t pad;
     unsigned long long coarse;  // phase 1: candidate leaves passing the wave-level test
-    unsigned long long fine;    // phase 1: candidate leaves staged and evaluated
+    unsigned long long fine;    // phase 1: candidate sub-boxes evaluated
+    uint32_t max_coarse, max_fine;
+    uint32_t hist[8];           // waves by coarse leaves: <16, <32, <64, <128, <256, <512, <1024, more
 };
 
 __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restrict__ sp, int P, int nleaves, int nsuper,
-                                                          const Box* __restrict__ leaves, const Box* __restrict__ supers,
+                                                          const Box* __restrict__ leaves, const Box* __restrict__ subs,
+                                                          const Box* __restrict__ supers,
                                                           float* __restrict__ out, uint32_t* __restrict__ hard,
-                                                          KnnCounters* __restrict__ counters)
+                                                          KnnCounters* __restrict__ counters,
+                                                          unsigned long long* __restrict__ trace, int stats)
 {
-    __shared__ __attribute__((aligned(16))) float4 s_pts[kWaves][kLeaf];
+    __shared__ uint32_t s_list[kWaves][kListCap];
+    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int wave = threadIdx.x / kWave;
     const int lane = lane_id();
     const int L = xcd_swizzle(blockIdx.x, gridDim.x) * kWaves + wave;
     if (L >= nleaves) return;  // whole wave exits; no workgroup barrier below
-    float4* stage = s_pts[wave];
 
     const int me = L * kLeaf + lane;
     const bool valid = me < P;
@@ -275,14 +381,7 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
     // seed from the own leaf
     {
         const int nc = min(kLeaf, P - L * kLeaf);
-        stage[lane] = valid ? p : make_float4(0.f, 0.f, 0.f, 0.f);
-        __builtin_amdgcn_wave_barrier();
-        for (int k = 0; k < nc; k++) {
-            const float4 c = stage[k];
-            const float d = sqdist(p, c);
-            if (k != lane) kbest(d, b0, b1, b2);
-        }
-        __builtin_amdgcn_wave_barrier();
+        for (int k0 = 0; k0 < nc; k0 += kChunk) eval_lanes(p, k0, nc, lane, p, b0, b1, b2);
     }
 
     // outliers -> phase 2
@@ -308,50 +407,149 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
     }
 
     if (__ballot(active)) {
-        const float4 qlo = make_float4(wave_min(active ? p.x : FLT_MAX), wave_min(active ? p.y : FLT_MAX),
-                                       wave_min(active ? p.z : FLT_MAX), 0.f);
-        const float4 qhi = make_float4(wave_max(active ? p.x : -FLT_MAX), wave_max(active ? p.y : -FLT_MAX),
-                                       wave_max(active ? p.z : -FLT_MAX), 0.f);
-        float ub = wave_max(active ? b2 : -FLT_MAX);
+        // Coarse filter against kGroups query groups (16 Morton-consecutive queries each, so a
+        // leaf that straddles a Morton jump does not inflate one wave-wide box): a box passes
+        // if it is within the group's upper bound of some group's box.  The walk is organised
+        // for memory-level parallelism: super-boxes are tested kSuperBatch per lane at a time,
+        // the leaf boxes of kLeafBatch passing super-boxes are loaded together, passing leaves
+        // go to an LDS list, and the list is evaluated with the next leaves' points and
+        // sub-boxes already in flight.
+        float4 glo[kGroups], ghi[kGroups];
+        float gub[kGroups];
+        group_boxes(p, active, glo, ghi);
+        group_bounds(b2, active, gub);
+        uint32_t* list = s_list[wave];
+        int nnear = 0, nfar = 0;  // list[0, nnear) near leaves, list[cap - nfar, cap) far leaves
         uint32_t n_coarse = 0, n_fine = 0;
-        for (int s0 = 0; s0 < nsuper; s0 += kWave) {
-            const int s = s0 + lane;
-            bool pass = false;
-            if (s < nsuper) {
-                const Box sb = supers[s];
-                pass = box_box_lb(sb, qlo, qhi) <= ub;
-            }
-            uint64_t smask = __ballot(pass);
-            while (smask) {
-                const int S = s0 + __builtin_ctzll(smask);
-                smask &= smask - 1;
-                const int l = S * kFan + lane;
-                bool lpass = false;
-                if (l < nleaves && l != L) {
-                    const Box lb = leaves[l];
-                    lpass = box_box_lb(lb, qlo, qhi) <= ub;
+
+        // evaluate and empty the candidate list
+        auto flush = [&]() {
+            const int cnt = nnear + nfar;
+            const int nn = nnear;
+            auto at = [&](int i) { return (int)list[i < nn ? i : kListCap - 1 - (i - nn)]; };
+            // prefetch ring: point (all lanes) and sub-box halves (lanes < 2 kSub) of leaves i+1, i+2
+            // Batches of kFlushBatch leaves: every point and sub-box load of a batch is issued before
+            // any is used, so a batch costs one memory latency.  (A rotating prefetch across
+            // iterations measured no gain: the waitcnt pass drains all loads at the loop header.)
+            for (int i0 = 0; i0 < cnt; i0 += kFlushBatch) {
+                float4 pt[kFlushBatch], bx[kFlushBatch];
+                int Cb[kFlushBatch];
+#pragma unroll
+                for (int q = 0; q < kFlushBatch; q++) {
+                    Cb[q] = at(min(i0 + q, cnt - 1));
+                    pt[q] = sp[min(Cb[q] * kLeaf + lane, P - 1)];
+                    bx[q] = reinterpret_cast<const float4*>(subs + (size_t)Cb[q] * kSub)[lane & (2 * kSub - 1)];
                 }
-                uint64_t lmask = __ballot(lpass);
-                while (lmask) {
-                    const int C = S * kFan + __builtin_ctzll(lmask);
-                    lmask &= lmask - 1;
-                    const Box cb = leaves[C];
+#pragma unroll
+                for (int q = 0; q < kFlushBatch; q++) {
+                    if (i0 + q >= cnt) break;
                     n_coarse++;
-                    if (!__ballot(active && box_point_lb(cb, p) <= b2)) continue;
-                    n_fine++;
-                    const int cbase = C * kLeaf;
-                    const int nc = min(kLeaf, P - cbase);
-                    stage[lane] = (lane < nc) ? sp[cbase + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    uint32_t smask4 = 0;
+#pragma unroll
+                    for (int j = 0; j < kSub; j++) {
+                        const Box sb{make_float4(uniform_lane(bx[q].x, 2 * j), uniform_lane(bx[q].y, 2 * j),
+                                                 uniform_lane(bx[q].z, 2 * j), 0.f),
+                                     make_float4(uniform_lane(bx[q].x, 2 * j + 1), uniform_lane(bx[q].y, 2 * j + 1),
+                                                 uniform_lane(bx[q].z, 2 * j + 1), 0.f)};
+                        if (__ballot(active && box_point_lb(sb, p) <= b2)) smask4 |= 1u << j;
+                    }
+                    const int nc = min(kLeaf, P - Cb[q] * kLeaf);
+                    while (smask4) {
+                        const int j = __builtin_ctz(smask4);
+                        smask4 &= smask4 - 1;
+                        n_fine++;
+                        eval_lanes(pt[q], j * kChunk, nc, -1, p, b0, b1, b2);
+                    }
+                }
+            }
+            nnear = nfar = 0;
+            group_bounds(b2, active, gub);
+        };
+
+        for (int s0 = 0; s0 < nsuper; s0 += kWave * kSuperBatch) {
+            uint64_t smask[kSuperBatch];
+            {
+                Box sb[kSuperBatch];
+#pragma unroll
+                for (int j = 0; j < kSuperBatch; j++) {
+                    const int sidx = s0 + j * kWave + lane;
+                    if (sidx < nsuper) sb[j] = supers[sidx];
+                }
+#pragma unroll
+                for (int j = 0; j < kSuperBatch; j++) {
+                    const int sidx = s0 + j * kWave + lane;
+                    bool pass = false;
+                    if (sidx < nsuper) {
+#pragma unroll
+                        for (int g = 0; g < kGroups; g++) pass |= box_box_lb(sb[j], glo[g], ghi[g]) <= gub[g];
+                    }
+                    smask[j] = __ballot(pass);
+                }
+            }
+            // passing super-boxes in ascending order, kLeafBatch at a time
+            int j = 0;
+            while (true) {
+                int S[kLeafBatch];
+                int ns = 0;
+                while (ns < kLeafBatch && j < kSuperBatch) {
+                    if (smask[j]) {
+                        S[ns++] = s0 + j * kWave + __builtin_ctzll(smask[j]);
+                        smask[j] &= smask[j] - 1;
+                    } else {
+                        j++;
+                    }
+                }
+                if (ns == 0) break;
+                Box lb[kLeafBatch];
+#pragma unroll
+                for (int q = 0; q < kLeafBatch; q++) {
+                    const int l = (q < ns ? S[q] : 0) * kFan + lane;
+                    if (q < ns && l < nleaves) lb[q] = leaves[l];
+                }
+#pragma unroll
+                for (int q = 0; q < kLeafBatch; q++) {
+                    if (q >= ns) break;
+                    const int l = S[q] * kFan + lane;
+                    bool lpass = false, near = false;
+                    if (l < nleaves && l != L) {
+#pragma unroll
+                        for (int g = 0; g < kGroups; g++) {
+                            const float d = box_box_lb(lb[q], glo[g], ghi[g]);
+                            lpass |= d <= gub[g];
+                            near |= d == 0.f;
+                        }
+                    }
+                    const uint64_t lm = __ballot(lpass);
+                    const int cnt = __popcll(lm);
+                    if (cnt == 0) continue;
+                    if (nnear + nfar + cnt > kListCap) flush();
+                    // leaves touching a query group's box go to the front and are evaluated first,
+                    // so the bounds shrink before the farther leaves are filtered
+                    const uint64_t nm = __ballot(lpass && near), fm = lm & ~nm;
+                    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+                    if (lpass && near) list[nnear + __popcll(nm & lt)] = (uint32_t)l;
+                    if (lpass && !near) list[kListCap - 1 - nfar - __popcll(fm & lt)] = (uint32_t)l;
+                    nnear += __popcll(nm);
+                    nfar += __popcll(fm);
                     __builtin_amdgcn_wave_barrier();
-                    for (int k = 0; k < nc; k++) kbest(sqdist(p, stage[k]), b0, b1, b2);
-                    __builtin_amdgcn_wave_barrier();
-                    ub = wave_max(active ? b2 : -FLT_MAX);
                 }
             }
         }
-        if (lane == 0) {
+        if (nnear + nfar) flush();
+        if (stats && lane == 0) {  // diagnostics only (HIDEGS_KNN_STATS): same-address atomics are slow
             atomicAdd(&counters->coarse, (unsigned long long)n_coarse);
             atomicAdd(&counters->fine, (unsigned long long)n_fine);
+            atomicMax(&counters->max_coarse, n_coarse);
+            atomicMax(&counters->max_fine, n_fine);
+            int bk = 0;
+            while (bk < 7 && n_coarse >= (16u << bk)) bk++;
+            atomicAdd(&counters->hist[bk], 1u);
+            if (trace) {
+                trace[4 * L + 0] = t_start;
+                trace[4 * L + 1] = __builtin_amdgcn_s_memrealtime();
+                trace[4 * L + 2] = n_coarse;
+                trace[4 * L + 3] = n_fine;
+            }
         }
     }
     if (active) out[__float_as_uint(p.w)] = ((b0 + b1) + b2) / 3.0f;
@@ -437,7 +635,7 @@ struct KnnLayout {
     void* sort_tmp;
     size_t sort_bytes;
     float4* sp;
-    Box *leaves, *supers;
+    Box *leaves, *subs, *supers;
     uint32_t* hard;
     KnnCounters* counters;
     float *partials, *params;
@@ -457,6 +655,7 @@ KnnLayout layout(void* base, int P)
     l.sort_tmp = c.take<char>(l.sort_bytes);
     l.sp = c.take<float4>(P);
     l.leaves = c.take<Box>(nleaves);
+    l.subs = c.take<Box>((size_t)nleaves * kSub);
     l.supers = c.take<Box>(nsuper);
     l.hard = c.take<uint32_t>(P);
     l.counters = c.take<KnnCounters>(1);
@@ -480,6 +679,10 @@ int dist_cuda2(hidegs_alloc_fn alloc, void* user, int P, const float* points, fl
     char* base = alloc(user, bytes);
     if (!base) return fail(HIDEGS_E_ALLOC, "distCUDA2: scratch allocation of " + std::to_string(bytes) + " bytes failed");
     const KnnLayout l = layout(base, P);
+    const char* stats_env = getenv("HIDEGS_KNN_STATS");
+    unsigned long long* trace = nullptr;
+    if (stats_env && *stats_env == '2') (void)hipMalloc(&trace, sizeof(unsigned long long) * 4 * ceil_div(P, kLeaf));
+    if (trace) (void)hipMemsetAsync(trace, 0, sizeof(unsigned long long) * 4 * ceil_div(P, kLeaf), stream);
     const int nleaves = ceil_div(P, kLeaf), nsuper = ceil_div(nleaves, kFan);
     const int nb = ceil_div(P, kBlock);
     const int nbound = std::min(kBoundBlocks, nb);
@@ -494,19 +697,50 @@ int dist_cuda2(hidegs_alloc_fn alloc, void* user, int P, const float* points, fl
     if (rc) return rc;
     HIDEGS_LAUNCH("gather", gather_kernel, dim3(nb), dim3(kBlock), 0, stream, points, l.vals_sorted, P, l.sp);
     HIDEGS_LAUNCH("leaf_box", leaf_box_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P, nleaves,
-                       l.leaves);
+                       l.leaves, l.subs);
     HIDEGS_LAUNCH("super_box", super_box_kernel, dim3(ceil_div(nsuper, kWaves)), dim3(kBlock), 0, stream, l.leaves, nleaves,
                        nsuper, l.supers);
     HIDEGS_LAUNCH("knn_leaf", knn_leaf_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P, nleaves,
-                       nsuper, l.leaves, l.supers, mean_dists, l.hard, l.counters);
+                       nsuper, l.leaves, l.subs, l.supers, mean_dists, l.hard, l.counters, trace,
+                  stats_env && *stats_env >= '1');
     HIDEGS_LAUNCH("knn_hard", knn_hard_kernel, dim3(std::min(2048, ceil_div(nleaves, kWaves))), dim3(kBlock), 0, stream, l.sp,
                        P, nleaves, nsuper, l.leaves, l.supers, mean_dists, l.hard, l.counters);
-    if (const char* e = getenv("HIDEGS_KNN_STATS"); e && *e == '1') {
+    if (trace) {
+        const int nl = ceil_div(P, kLeaf);
+        std::vector<unsigned long long> h(4 * (size_t)nl);
+        (void)hipMemcpyAsync(h.data(), trace, h.size() * 8, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        (void)hipFree(trace);
+        unsigned long long t0 = ~0ull, t1 = 0;
+        std::vector<double> dur;
+        for (int i = 0; i < nl; i++)
+            if (h[4 * i + 1]) {
+                t0 = std::min(t0, h[4 * i]);
+                t1 = std::max(t1, h[4 * i + 1]);
+                dur.push_back((double)(h[4 * i + 1] - h[4 * i]));
+            }
+        std::sort(dur.begin(), dur.end());
+        auto pct = [&](double q) { return dur.empty() ? 0.0 : dur[(size_t)(q * (dur.size() - 1))] / 100.0; };
+        double sum = 0;
+        for (double d : dur) sum += d;
+        fprintf(stderr, "[hidegs knn trace] waves=%zu span=%.1f us sum=%.1f us avg-concurrency=%.1f "
+                "dur us p50=%.2f p90=%.2f p99=%.2f p999=%.2f max=%.2f\n", dur.size(), (t1 - t0) / 100.0, sum / 100.0,
+                sum / std::max(1.0, (double)(t1 - t0)), pct(0.5), pct(0.9), pct(0.99), pct(0.999), pct(1.0));
+        // start-time profile: waves started per 10% of the span
+        int bins[10] = {0};
+        for (int i = 0; i < nl; i++)
+            if (h[4 * i + 1]) bins[std::min(9, (int)(10.0 * (h[4 * i] - t0) / std::max(1ull, t1 - t0)))]++;
+        fprintf(stderr, "[hidegs knn trace] starts per tenth: %d %d %d %d %d %d %d %d %d %d\n", bins[0], bins[1],
+                bins[2], bins[3], bins[4], bins[5], bins[6], bins[7], bins[8], bins[9]);
+    }
+    if (const char* e = getenv("HIDEGS_KNN_STATS"); e && *e >= '1') {
         KnnCounters h{};
         if (hipMemcpyAsync(&h, l.counters, sizeof(h), hipMemcpyDeviceToHost, stream) == hipSuccess &&
             hipStreamSynchronize(stream) == hipSuccess)
-            fprintf(stderr, "[hidegs knn] P=%d leaves=%d supers=%d hard=%u coarse_leaves/wave=%.2f fine_leaves/wave=%.2f\n",
-                    P, nleaves, nsuper, h.hard, (double)h.coarse / nleaves, (double)h.fine / nleaves);
+            fprintf(stderr, "[hidegs knn] P=%d leaves=%d supers=%d hard=%u coarse_leaves/wave=%.2f (max %u) "
+                    "sub_boxes/wave=%.2f (max %u) hist<16,32,64,128,256,512,1024,more: %u %u %u %u %u %u %u %u\n",
+                    P, nleaves, nsuper, h.hard, (double)h.coarse / nleaves, h.max_coarse, (double)h.fine / nleaves,
+                    h.max_fine, h.hist[0], h.hist[1], h.hist[2], h.hist[3], h.hist[4], h.hist[5], h.hist[6], h.hist[7]);
     }
     return check_launch("distCUDA2", stream, 0);
 }

@@ -4,7 +4,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["HIDEGS_KNN_STATS"] = "1"
+os.environ["HIDEGS_KNN_STATS"] = "2"
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -27,4 +27,4 @@ for name, pts in sets.items():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t
         print(name, f"total {dt*1e3:.2f} ms", {k: round(kt.get(k)[0] * 1e3, 1) for k in ("knn_leaf", "knn_hard", "radix_scatter_u64")}, flush=True)
-    os.environ["HIDEGS_KNN_STATS"] = "1"
+    os.environ["HIDEGS_KNN_STATS"] = "2"
