@@ -54,6 +54,8 @@ SIGNATURES = {
     "hidegs_sort_pairs_u32": (I, [P, SZ, P, P, P, P, LL, I, I, P]),
     "hidegs_identify_tile_ranges": (I, [P, LL, P, I, P]),
     "hidegs_higher_msb": (U32, [U32]),
+    "hidegs_masked_adam": (I, [P, P, P, P, P, LL, I, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
+                                LL, P]),
     "hidegs_kernel_timing": (None, [I]),
     "hidegs_kernel_timing_reset": (None, []),
     "hidegs_kernel_time": (I, [C.c_char_p, P, P]),

@@ -18,7 +18,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(HERE, "..", "include")
 OBJDIR = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libhidegs.so")
-SOURCES = ["abi.cpp", "timing.cpp", "primitives.hip", "knn.hip"]
+SOURCES = ["abi.cpp", "timing.cpp", "primitives.hip", "knn.hip", "adam.hip"]
 HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(INCLUDE, "hidegs.h")]
 
 # -ffp-contract=off: every fused multiply-add in the kernels is an explicit fmaf, so the

@@ -22,6 +22,8 @@
  *                                  SK/simple_knn.cu:211-214)
  *   hidegs_identify_tile_ranges <- cudaMemsetAsync(ranges) + identifyTileRanges (HR/cuda_rasterizer/rasterizer_impl.cu:364-371,120-142)
  *   hidegs_higher_msb           <- getHigherMsb (HR/cuda_rasterizer/rasterizer_impl.cu:35-50)
+ *   hidegs_masked_adam          <- the per-parameter update of scene/OurAdam.py (_single_tensor_adam :249-337,
+ *                                  _single_tensor_adam2 :340-420)
  * INTEGRATION.md shows the Python-side bindings.
  */
 #ifndef HIDEGS_H_INCLUDED
@@ -138,6 +140,18 @@ int hidegs_identify_tile_ranges(const uint64_t* sorted_keys, long long n, uint32
 
 /* [host] getHigherMsb: bits needed to hold n, at least 1; the sort end bit is 32 + this of the tile count. */
 uint32_t hidegs_higher_msb(uint32_t n);
+
+/*
+ * Fused row-masked Adam step on one fp32 parameter of rows x width values (row-major).  Rows
+ * with relevant[r] != 0 -- every row when relevant is NULL (the reference's empty-mask path) --
+ * are updated exactly as OurAdam's torch ops update them on this GPU (op order and rounding in
+ * hidegs_amd/csrc/adam.hip); other rows are neither read nor written.  `step` is the
+ * parameter's step count after this call's increment (>= 1); lr, betas, eps, weight_decay are
+ * the Python doubles the reference passes.  param, exp_avg, exp_avg_sq are updated in place.
+ */
+int hidegs_masked_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                       const unsigned char* relevant, long long rows, int width, double lr, double beta1,
+                       double beta2, double eps, double weight_decay, long long step, void* stream);
 
 /*
  * [host] Per-kernel device timing.  While enabled, every kernel this library launches is

@@ -5,6 +5,7 @@ the checker or the timed CPU baseline.  The product packages (diff_gaussian_rast
 simple_knn, hidegs_amd) never import it.
 
   knn_mean3 / knn_mean3_subset  -- distCUDA2's value from its definition (knn_ref.c)
+  masked_adam                   -- one OurAdam step on one parameter tensor (adam_ref.c)
   stable_sort_pairs / inclusive_scan_u32 / tile_ranges -- generic integer restatements
      of the binning primitives (numpy), see binning.py
 """
@@ -36,6 +37,9 @@ def lib() -> C.CDLL:
         dll.oracle_knn_mean3.restype = None
         dll.oracle_knn_mean3_subset.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_longlong, C.c_void_p]
         dll.oracle_knn_mean3_subset.restype = None
+        dll.oracle_masked_adam.argtypes = [C.c_void_p] * 5 + [C.c_longlong, C.c_int] + [C.c_double] * 5 + \
+            [C.c_longlong]
+        dll.oracle_masked_adam.restype = None
         _lib = dll
     return _lib
 
@@ -57,3 +61,18 @@ def knn_mean3_subset(points: np.ndarray, idx: np.ndarray) -> np.ndarray:
     if ii.shape[0]:
         lib().oracle_knn_mean3_subset(pts.ctypes.data, pts.shape[0], ii.ctypes.data, ii.shape[0], out.ctypes.data)
     return out
+
+
+def masked_adam(param, grad, exp_avg, exp_avg_sq, relevant, lr, beta1=0.9, beta2=0.999, eps=1e-8,
+                weight_decay=0.0, step=1):
+    """One OurAdam step on float32 arrays (rows, ...) updated in place; relevant: bool (rows,) or None."""
+    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (param, grad, exp_avg, exp_avg_sq)]
+    for a, orig in zip(arrs, (param, grad, exp_avg, exp_avg_sq)):
+        if a is not orig:
+            raise ValueError("arrays must be contiguous float32 (updated in place)")
+    rows = param.shape[0]
+    width = int(np.prod(param.shape[1:])) if param.ndim > 1 else 1
+    rel = None if relevant is None else np.ascontiguousarray(relevant, dtype=np.uint8)
+    lib().oracle_masked_adam(param.ctypes.data, grad.ctypes.data, exp_avg.ctypes.data, exp_avg_sq.ctypes.data,
+                             None if rel is None else rel.ctypes.data, rows, width, lr, beta1, beta2, eps,
+                             weight_decay, int(step))
