@@ -363,80 +363,50 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
 // read/write of every pair.
 
 constexpr int kSegCap = 2048;
+constexpr int kSegRounds = kSegCap / kBlock;  // rounds of 64 per wave
 
-// One WAVE per segment (kSegWaves segments per workgroup, no workgroup barrier anywhere): the
-// segment's low key halves and indices live in registers, item i at (lane i % 64, slot i / 64);
-// each LSD pass ranks them with wave_rank, scans the 256 digit counts across the wave, and
-// permutes through a wave-private LDS buffer (4 B key + 2 B index per item).  Full keys and
-// values are gathered by original index from the partitioned input (src) and written to the
-// output (dst), so no register or LDS copy of the full pairs is needed.
-constexpr int kSegWaves = 4;
-
-__device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t* total)
-{
-    const int lane = lane_id();
-    uint32_t inc = v;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t o = __shfl_up(inc, d, kWave);
-        if (lane >= d) inc += o;
-    }
-    *total = __shfl(inc, kWave - 1, kWave);
-    return inc - v;
-}
-
-// Two instantiations split the segments by size: kSegSlots = 16 takes m <= 1024, kSegSlots = 32
-// takes 1024 < m <= 2048 (fewer registers and more waves per CU for the common small tiles).
-template <int kSegSlots>
-__global__ __launch_bounds__(kBlock) void segment_sort_kernel(const uint64_t* __restrict__ keys,
-                                                              const uint32_t* __restrict__ vals,
-                                                              uint64_t* __restrict__ keys_out,
-                                                              uint32_t* __restrict__ vals_out,
-                                                              const uint2* __restrict__ ranges, int nseg,
+__global__ __launch_bounds__(kBlock) void segment_sort_kernel(uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                              const uint2* __restrict__ ranges,
                                                               uint32_t* __restrict__ overflow,
                                                               uint32_t* __restrict__ n_overflow)
 {
-    constexpr int kCap = kSegSlots * kWave;
-    __shared__ __attribute__((aligned(16))) uint32_t s_key[kSegWaves][kCap];
-    __shared__ __attribute__((aligned(16))) uint16_t s_idx[kSegWaves][kCap];
-    __shared__ uint32_t s_cnt[kSegWaves][kRadix];
-    const int wave = threadIdx.x / kWave;
-    const int lane = lane_id();
-    const int seg = blockIdx.x * kSegWaves + wave;
-    if (seg >= nseg) return;
-    const uint2 r = ranges[seg];
-    if (r.y <= r.x) return;  // absent
-    const uint32_t begin = r.x, m = r.y - r.x;
-    if (kSegSlots == 16 && m == 1) {
-        if (lane == 0) {
-            keys_out[begin] = keys[begin];
-            vals_out[begin] = vals[begin];
-        }
-        return;
-    }
-    if (kSegSlots == 16 && m > (uint32_t)kCap) return;                        // the 32-slot launch's
-    if (kSegSlots == 32 && (m <= (uint32_t)kCap / 2 || m > (uint32_t)kCap)) {  // or nobody's
-        if (m > (uint32_t)kCap && lane == 0) overflow[atomicAdd(n_overflow, 1u)] = seg;
-        return;
-    }
-    const int slots = (int)((m + kWave - 1) / kWave);  // wave-uniform
-    uint32_t* cnt = s_cnt[wave];
-    uint32_t* sk = s_key[wave];
-    uint16_t* si = s_idx[wave];
+    // LDS holds (low 32 key bits, original index) pairs; the full keys and values stay in
+    // registers and are exchanged through LDS once, by original index, after the last pass.
+    __shared__ __attribute__((aligned(16))) uint32_t s_k[2][kSegCap];
+    __shared__ __attribute__((aligned(16))) uint32_t s_i[2][kSegCap];
+    __shared__ uint32_t s_cnt[kWavesPerBlock][kRadix];
+    __shared__ uint32_t s_start[kRadix];
+    __shared__ uint32_t s_wave[kWavesPerBlock];
+    __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock];
 
-    uint32_t k[kSegSlots], id[kSegSlots];
+    const int t = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = t / kWave;
+    const uint2 r = ranges[blockIdx.x];
+    const uint32_t begin = r.x, m = r.y - r.x;
+    if (r.y <= r.x + 1) return;  // absent or single pair: already in place
+    if (m > (uint32_t)kSegCap) {
+        if (t == 0) overflow[atomicAdd(n_overflow, 1u)] = blockIdx.x;
+        return;
+    }
+    // all loads issued before any is used: item t + 256 q
+    uint64_t kin[kSegRounds];
+    uint32_t vin[kSegRounds];
+#pragma unroll
+    for (int q = 0; q < kSegRounds; q++) {
+        const uint32_t i = t + q * kBlock;
+        kin[q] = i < m ? keys[begin + i] : 0ull;
+        vin[q] = i < m ? vals[begin + i] : 0u;
+    }
     uint32_t a = 0xffffffffu, o = 0;
 #pragma unroll
-    for (int q = 0; q < kSegSlots; q++) {
-        const uint32_t i = q * kWave + lane;
-        if (q < slots) {
-            const bool ok = i < m;
-            k[q] = ok ? (uint32_t)keys[begin + i] : 0u;
-            id[q] = i;
-            if (ok) {
-                a &= k[q];
-                o |= k[q];
-            }
+    for (int q = 0; q < kSegRounds; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            s_k[0][i] = (uint32_t)kin[q];
+            s_i[0][i] = i;
+            a &= (uint32_t)kin[q];
+            o |= (uint32_t)kin[q];
         }
     }
 #pragma unroll
@@ -444,73 +414,93 @@ __global__ __launch_bounds__(kBlock) void segment_sort_kernel(const uint64_t* __
         a &= __shfl_xor(a, sh, kWave);
         o |= __shfl_xor(o, sh, kWave);
     }
-    const uint32_t diff = a ^ o;  // bits that vary over the segment
-
+    if (lane == 0) {
+        s_and[wave] = a;
+        s_or[wave] = o;
+    }
+    __syncthreads();
+    uint32_t diff;
+    {
+        uint32_t aa = 0xffffffffu, oo = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; w++) {
+            aa &= s_and[w];
+            oo |= s_or[w];
+        }
+        diff = aa ^ oo;  // bits that vary over the segment
+    }
+    // wave w ranks items [w*C, w*C + C) in (round, lane) order; C is a multiple of 64
+    const uint32_t C = ((m + kBlock - 1) / kBlock) * kWave;
+    const int rounds = (int)(C / kWave);
+    const uint32_t w0 = wave * C;
+    int cur = 0;
     for (int shift = 0; shift < 32; shift += kRadixBits) {
         if (((diff >> shift) & (kRadix - 1)) == 0) continue;  // digit constant over the segment
+        for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t k[kSegRounds], id[kSegRounds], rank[kSegRounds];
+        bool ok[kSegRounds];
 #pragma unroll
-        for (int j = 0; j < kRadix / kWave; j++) cnt[j * kWave + lane] = 0;
-        __builtin_amdgcn_wave_barrier();
-        uint32_t rank[kSegSlots];
+        for (int q = 0; q < kSegRounds; q++) {
+            const uint32_t i = w0 + q * kWave + lane;
+            ok[q] = q < rounds && i < m;
+            k[q] = ok[q] ? s_k[cur][i] : 0u;
+            id[q] = ok[q] ? s_i[cur][i] : 0u;
+        }
+        // the ranking of rounds >= `rounds` is skipped as a whole (block-uniform)
+        if (rounds == kSegRounds) {
+            wave_rank<uint32_t, kSegRounds>(k, ok, shift, kRadix - 1, s_cnt[wave], rank);
+        } else {
 #pragma unroll
-        for (int q = 0; q < kSegSlots; q++) {
-            if (q < slots) {
-                uint32_t kk[1] = {k[q]}, rr[1];
-                bool oo[1] = {q * kWave + lane < (int)m};
-                wave_rank<uint32_t, 1>(kk, oo, shift, kRadix - 1, cnt, rr);
-                rank[q] = rr[0];
+            for (int q = 0; q < kSegRounds; q++) {
+                if (q < rounds) {
+                    uint32_t kk[1] = {k[q]}, rr[1];
+                    bool oo[1] = {ok[q]};
+                    wave_rank<uint32_t, 1>(kk, oo, shift, kRadix - 1, s_cnt[wave], rr);
+                    rank[q] = rr[0];
+                }
             }
         }
-        __builtin_amdgcn_wave_barrier();
-        // exclusive scan of the 256 digit counts: lane holds digits 4 lane .. 4 lane + 3
-        uint32_t c4[kRadix / kWave], sum = 0;
+        __syncthreads();
+        const uint32_t tot = digit_wave_prefix(s_cnt);
+        uint32_t dummy;
+        s_start[t] = block_exclusive_scan(tot, s_wave, &dummy);
+        __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kRadix / kWave; j++) {
-            c4[j] = cnt[lane * (kRadix / kWave) + j];
-            sum += c4[j];
-        }
-        uint32_t tot;
-        uint32_t run = wave_exclusive_scan(sum, &tot);
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int j = 0; j < kRadix / kWave; j++) {
-            cnt[lane * (kRadix / kWave) + j] = run;
-            run += c4[j];
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int q = 0; q < kSegSlots; q++) {
-            if (q < slots && q * kWave + lane < (int)m) {
-                const uint32_t pos = cnt[digit_of(k[q], shift, kRadix - 1)] + rank[q];
-                sk[pos] = k[q];
-                si[pos] = (uint16_t)id[q];
+        for (int q = 0; q < kSegRounds; q++) {
+            if (ok[q]) {
+                const uint32_t dd = digit_of(k[q], shift, kRadix - 1);
+                const uint32_t pos = s_start[dd] + s_cnt[wave][dd] + rank[q];
+                s_k[cur ^ 1][pos] = k[q];
+                s_i[cur ^ 1][pos] = id[q];
             }
         }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int q = 0; q < kSegSlots; q++) {
-            const uint32_t i = q * kWave + lane;
-            if (q < slots && i < m) {
-                k[q] = sk[i];
-                id[q] = si[i];
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
+        cur ^= 1;
     }
-    // gather the full pairs by original index from the partitioned input
+    // exchange full keys (high half) and values by original index through the free buffer
 #pragma unroll
-    for (int q = 0; q < kSegSlots; q++) {
-        const uint32_t i = q * kWave + lane;
-        if (q < slots && i < m) {
-            keys_out[begin + i] = keys[begin + id[q]];
-            vals_out[begin + i] = vals[begin + id[q]];
+    for (int q = 0; q < kSegRounds; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            s_k[cur ^ 1][i] = (uint32_t)(kin[q] >> 32);
+            s_i[cur ^ 1][i] = vin[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kSegRounds; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            const uint32_t src = s_i[cur][i];
+            keys[begin + i] = ((uint64_t)s_k[cur ^ 1][src] << 32) | s_k[cur][i];
+            vals[begin + i] = s_i[cur ^ 1][src];
         }
     }
 }
 
 // One workgroup per oversized segment: 4 stable LSD passes over the low 32 bits through
-// global memory within the segment's range, partitioned input (alt) -> out -> alt -> out -> alt,
-// then one copy to out; 4096 items per step.
+// global memory (keys/vals <-> alt within the segment's range), 4096 items per step.
 __global__ __launch_bounds__(kBlock) void segment_sort_big_kernel(uint64_t* __restrict__ keys,
                                                                   uint32_t* __restrict__ vals,
                                                                   uint64_t* __restrict__ alt_k,
@@ -532,10 +522,10 @@ __global__ __launch_bounds__(kBlock) void segment_sort_big_kernel(uint64_t* __re
         const uint32_t begin = r.x, m = r.y - r.x;
         for (int pass = 0; pass < 4; pass++) {
             const int shift = pass * kRadixBits;
-            const uint64_t* sk = (pass & 1) ? keys : alt_k;
-            const uint32_t* sv = (pass & 1) ? vals : alt_v;
-            uint64_t* dk = (pass & 1) ? alt_k : keys;
-            uint32_t* dv = (pass & 1) ? alt_v : vals;
+            const uint64_t* sk = (pass & 1) ? alt_k : keys;
+            const uint32_t* sv = (pass & 1) ? alt_v : vals;
+            uint64_t* dk = (pass & 1) ? keys : alt_k;
+            uint32_t* dv = (pass & 1) ? vals : alt_v;
             s_hist[t] = 0;
             __syncthreads();
             for (uint32_t i = t; i < m; i += kBlock) atomicAdd(&s_hist[digit_of(sk[begin + i], shift, kRadix - 1)], 1u);
@@ -576,11 +566,6 @@ __global__ __launch_bounds__(kBlock) void segment_sort_big_kernel(uint64_t* __re
                 __syncthreads();
             }
         }
-        for (uint32_t i = t; i < m; i += kBlock) {  // the 4th pass left the segment in alt
-            keys[begin + i] = alt_k[begin + i];
-            vals[begin + i] = alt_v[begin + i];
-        }
-        __syncthreads();
     }
 }
 
@@ -677,9 +662,7 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         const int shift = lo_bit + p * kRadixBits;
         const int bits = (end_bit - shift) < kRadixBits ? (end_bit - shift) : kRadixBits;
         const uint32_t mask = (1u << bits) - 1u;
-        // plain sort: the last pass lands in out; segmented: it lands in alt, and the per-segment
-        // sort reads alt and writes out
-        const bool to_out = ((lsd_passes - 1 - p) % 2) == (segmented ? 1 : 0);
+        const bool to_out = ((lsd_passes - 1 - p) % 2) == 0;
         K* dk = to_out ? keys_out : alt_k;
         uint32_t* dv = to_out ? vals_out : alt_v;
         HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_hist_u64" : "radix_hist_u32"), radix_hist_kernel<K>, dim3(nt),
@@ -700,17 +683,12 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         if (hipMemsetAsync(ranges, 0, sizeof(uint2) * nseg, stream) != hipSuccess ||
             hipMemsetAsync(n_overflow, 0, sizeof(uint32_t), stream) != hipSuccess)
             return fail(HIDEGS_E_HIP, std::string(what) + ": memset failed");
-        uint64_t* ak = reinterpret_cast<uint64_t*>(alt_k);
         HIDEGS_LAUNCH("segment_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock)), dim3(kBlock), 0, stream,
-                      (const uint64_t*)ak, n, ranges, (uint32_t)nseg, (uint32_t)(nseg - 1));
-        HIDEGS_LAUNCH("segment_sort", segment_sort_kernel<16>, dim3(ceil_div(nseg, kSegWaves)), dim3(kBlock), 0,
-                      stream, (const uint64_t*)ak, (const uint32_t*)alt_v, ko, vals_out, ranges, nseg, overflow,
-                      n_overflow);
-        HIDEGS_LAUNCH("segment_sort_2k", segment_sort_kernel<32>, dim3(ceil_div(nseg, kSegWaves)), dim3(kBlock), 0,
-                      stream, (const uint64_t*)ak, (const uint32_t*)alt_v, ko, vals_out, ranges, nseg, overflow,
-                      n_overflow);
+                      (const uint64_t*)ko, n, ranges, (uint32_t)nseg, (uint32_t)(nseg - 1));
+        HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out, ranges,
+                      overflow, n_overflow);
         HIDEGS_LAUNCH("segment_sort_big", segment_sort_big_kernel, dim3(nseg < 512 ? nseg : 512), dim3(kBlock), 0,
-                      stream, ko, vals_out, ak, alt_v, ranges, overflow, n_overflow);
+                      stream, ko, vals_out, reinterpret_cast<uint64_t*>(alt_k), alt_v, ranges, overflow, n_overflow);
     }
     return check_launch(what, stream, 0);
 }
