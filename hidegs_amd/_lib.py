@@ -13,7 +13,8 @@ import threading
 
 import torch  # noqa: F401  -- load torch's HIP runtime first; libhidegs binds to the same libamdhip64.so.7
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhidegs.so")
+# HIDEGS_LIB selects another build of the same ABI (tools/build_variant.py experiments)
+LIB_PATH = os.environ.get("HIDEGS_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhidegs.so")
 
 E_ARG, E_HIP, E_ALLOC, E_UNSUPPORTED = -1, -2, -3, -4
 

@@ -356,32 +356,120 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
 // Keys whose bits [32, end_bit) are a small segment id -- the (tile | depth) keys of the
 // binning stage -- are sorted in two stages with the same result as the LSD sort over
 // [0, end_bit): (1) the LSD passes above over [32, end_bit) only, which partition the pairs
-// stably by segment; (2) one workgroup per segment sorts it stably by the low 32 bits in LDS
-// (passes whose digit is constant over the segment are skipped).  Segments larger than
-// kSegCap go to a list that a second kernel sorts with one workgroup each, through global
-// memory, 4096 items at a time.  Global traffic drops from 6 LSD passes to 2 plus one
-// read/write of every pair.
+// stably by segment; (2) one workgroup per segment sorts it stably by the low 32 bits in LDS.
+// Global traffic drops from 6 LSD passes to 2 plus one read/write of every pair.
+//
+// Stage (2) is latency-bound (a tile holds ~1000 pairs), so the workgroup's LDS is sized for
+// one run of kSegRun pairs (~21 KB, 7 workgroups per CU).  A segment of up to kSegCap pairs
+// is sorted as two runs, the first parked in registers while the second is sorted, and the
+// runs are merged by rank (binary search in LDS).  Larger segments go to a list that a second
+// kernel sorts through global memory.
 
-constexpr int kSegCap = 2048;
-constexpr int kSegRounds = kSegCap / kBlock;  // rounds of 64 per wave
+#ifndef HIDEGS_SEG_BITS
+#define HIDEGS_SEG_BITS 32  // experiments only (tools/build_variant.py): fewer bits give wrong orders
+#endif
+constexpr int kSegRun = 1024;            // pairs per LDS-sorted run
+constexpr int kSegCap = 2 * kSegRun;     // largest segment sorted by segment_sort_kernel
+constexpr int kRunItems = kSegRun / kBlock;  // run items per thread (rounds of 64 per wave)
+constexpr int kSegItems = kSegCap / kBlock;  // segment items per thread
 
-__global__ __launch_bounds__(kBlock) void segment_sort_kernel(uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                              const uint2* __restrict__ ranges,
-                                                              uint32_t* __restrict__ overflow,
-                                                              uint32_t* __restrict__ n_overflow)
+// LDS of one workgroup: two (low key, index-in-segment) buffers of one run plus ranking state.
+struct SegShared {
+    uint32_t k[2][kSegRun];
+    uint32_t i[2][kSegRun];
+    uint32_t cnt[kWavesPerBlock][kRadix];
+    uint32_t start[kRadix];
+    uint32_t wave[kWavesPerBlock];
+};
+
+// Stable LSD sort of the n <= kSegRun (k, i) pairs in buffer 0 by the key bits set in `diff`
+// (8-bit digits; a digit that is constant over the segment is skipped).  Returns the buffer
+// holding the result.  Wave w ranks items [w*C, w*C + C) in (round, lane) order.
+__device__ __forceinline__ int lds_radix_sort(SegShared& sh, const uint32_t n, const uint32_t diff)
 {
-    // LDS holds (low 32 key bits, original index) pairs; the full keys and values stay in
-    // registers and are exchanged through LDS once, by original index, after the last pass.
-    __shared__ __attribute__((aligned(16))) uint32_t s_k[2][kSegCap];
-    __shared__ __attribute__((aligned(16))) uint32_t s_i[2][kSegCap];
-    __shared__ uint32_t s_cnt[kWavesPerBlock][kRadix];
-    __shared__ uint32_t s_start[kRadix];
-    __shared__ uint32_t s_wave[kWavesPerBlock];
-    __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock];
+    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
+    const uint32_t C = ((n + kBlock - 1) / kBlock) * kWave;
+    const int rounds = (int)(C / kWave);
+    const uint32_t w0 = wave * C;
+    int cur = 0;
+    for (int shift = 0; shift < HIDEGS_SEG_BITS; shift += kRadixBits) {
+        if (((diff >> shift) & (kRadix - 1)) == 0) continue;  // block-uniform
+        for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&sh.cnt[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t k[kRunItems], id[kRunItems], rank[kRunItems];
+        bool ok[kRunItems];
+#pragma unroll
+        for (int q = 0; q < kRunItems; q++) {
+            const uint32_t i = w0 + q * kWave + lane;
+            ok[q] = q < rounds && i < n;
+            k[q] = ok[q] ? sh.k[cur][i] : 0u;
+            id[q] = ok[q] ? sh.i[cur][i] : 0u;
+        }
+        if (rounds == kRunItems) {
+            wave_rank<uint32_t, kRunItems>(k, ok, shift, kRadix - 1, sh.cnt[wave], rank);
+        } else {  // rounds past `rounds` hold no item: skip their ranking (block-uniform)
+#pragma unroll
+            for (int q = 0; q < kRunItems; q++) {
+                if (q < rounds) {
+                    uint32_t kk[1] = {k[q]}, rr[1];
+                    bool oo[1] = {ok[q]};
+                    wave_rank<uint32_t, 1>(kk, oo, shift, kRadix - 1, sh.cnt[wave], rr);
+                    rank[q] = rr[0];
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t tot = digit_wave_prefix(sh.cnt);
+        uint32_t dummy;
+        sh.start[t] = block_exclusive_scan(tot, sh.wave, &dummy);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kRunItems; q++) {
+            if (ok[q]) {
+                const uint32_t dd = digit_of(k[q], shift, kRadix - 1);
+                const uint32_t pos = sh.start[dd] + sh.cnt[wave][dd] + rank[q];
+                sh.k[cur ^ 1][pos] = k[q];
+                sh.i[cur ^ 1][pos] = id[q];
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    return cur;
+}
 
-    const int t = threadIdx.x;
-    const int lane = lane_id();
-    const int wave = t / kWave;
+// Number of the n sorted keys in a[] that are < key (or <= key when `inclusive`).
+__device__ __forceinline__ uint32_t lds_rank(const uint32_t* a, uint32_t n, uint32_t key, bool inclusive)
+{
+    uint32_t lo = 0, len = n;
+    while (len > 0) {
+        const uint32_t half = len >> 1;
+        const uint32_t v = a[lo + half];
+        const bool go_right = inclusive ? (v <= key) : (v < key);
+        lo = go_right ? lo + half + 1 : lo;
+        len = go_right ? len - half - 1 : half;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void wave_and_or(uint32_t& a, uint32_t& o)
+{
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        a &= __shfl_xor(a, sh, kWave);
+        o |= __shfl_xor(o, sh, kWave);
+    }
+}
+
+// Workgroup b sorts segment b (<= kSegCap pairs) in place by the low 32 key bits; larger
+// segments are appended to `overflow`.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void segment_sort_kernel(
+    uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint2* __restrict__ ranges,
+    uint32_t* __restrict__ overflow, uint32_t* __restrict__ n_overflow)
+{
+    __shared__ __attribute__((aligned(16))) SegShared sh;
+    __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock];
+    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
     const uint2 r = ranges[blockIdx.x];
     const uint32_t begin = r.x, m = r.y - r.x;
     if (r.y <= r.x + 1) return;  // absent or single pair: already in place
@@ -389,31 +477,27 @@ __global__ __launch_bounds__(kBlock) void segment_sort_kernel(uint64_t* __restri
         if (t == 0) overflow[atomicAdd(n_overflow, 1u)] = blockIdx.x;
         return;
     }
-    // all loads issued before any is used: item t + 256 q
-    uint64_t kin[kSegRounds];
-    uint32_t vin[kSegRounds];
-#pragma unroll
-    for (int q = 0; q < kSegRounds; q++) {
-        const uint32_t i = t + q * kBlock;
-        kin[q] = i < m ? keys[begin + i] : 0ull;
-        vin[q] = i < m ? vals[begin + i] : 0u;
-    }
+    const uint32_t na = m < (uint32_t)kSegRun ? m : (uint32_t)kSegRun, nb = m - na;
+    // low key halves: run A into LDS buffer 0, run B into registers; bits that vary
+    uint32_t bk[kRunItems];
     uint32_t a = 0xffffffffu, o = 0;
 #pragma unroll
-    for (int q = 0; q < kSegRounds; q++) {
+    for (int q = 0; q < kRunItems; q++) {
         const uint32_t i = t + q * kBlock;
-        if (i < m) {
-            s_k[0][i] = (uint32_t)kin[q];
-            s_i[0][i] = i;
-            a &= (uint32_t)kin[q];
-            o |= (uint32_t)kin[q];
+        const uint32_t ka = i < na ? (uint32_t)keys[begin + i] : 0u;
+        bk[q] = i < nb ? (uint32_t)keys[begin + kSegRun + i] : 0u;
+        if (i < na) {
+            sh.k[0][i] = ka;
+            sh.i[0][i] = i;
+            a &= ka;
+            o |= ka;
+        }
+        if (i < nb) {
+            a &= bk[q];
+            o |= bk[q];
         }
     }
-#pragma unroll
-    for (int sh = 32; sh >= 1; sh >>= 1) {
-        a &= __shfl_xor(a, sh, kWave);
-        o |= __shfl_xor(o, sh, kWave);
-    }
+    wave_and_or(a, o);
     if (lane == 0) {
         s_and[wave] = a;
         s_or[wave] = o;
@@ -429,72 +513,76 @@ __global__ __launch_bounds__(kBlock) void segment_sort_kernel(uint64_t* __restri
         }
         diff = aa ^ oo;  // bits that vary over the segment
     }
-    // wave w ranks items [w*C, w*C + C) in (round, lane) order; C is a multiple of 64
-    const uint32_t C = ((m + kBlock - 1) / kBlock) * kWave;
-    const int rounds = (int)(C / kWave);
-    const uint32_t w0 = wave * C;
-    int cur = 0;
-    for (int shift = 0; shift < 32; shift += kRadixBits) {
-        if (((diff >> shift) & (kRadix - 1)) == 0) continue;  // digit constant over the segment
-        for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
-        __syncthreads();
-        uint32_t k[kSegRounds], id[kSegRounds], rank[kSegRounds];
-        bool ok[kSegRounds];
+    const int ca = lds_radix_sort(sh, na, diff);
+
+    // final (position, low key, index) of this thread's items: position t + 256 q
+    uint32_t fk[kSegItems], fi[kSegItems], fp[kSegItems];
+    bool fok[kSegItems];
+    if (nb == 0) {
 #pragma unroll
-        for (int q = 0; q < kSegRounds; q++) {
-            const uint32_t i = w0 + q * kWave + lane;
-            ok[q] = q < rounds && i < m;
-            k[q] = ok[q] ? s_k[cur][i] : 0u;
-            id[q] = ok[q] ? s_i[cur][i] : 0u;
+        for (int q = 0; q < kSegItems; q++) {
+            const uint32_t i = t + q * kBlock;
+            fok[q] = q < kRunItems && i < na;
+            fp[q] = i;
+            fk[q] = fok[q] ? sh.k[ca][i] : 0u;
+            fi[q] = fok[q] ? sh.i[ca][i] : 0u;
         }
-        // the ranking of rounds >= `rounds` is skipped as a whole (block-uniform)
-        if (rounds == kSegRounds) {
-            wave_rank<uint32_t, kSegRounds>(k, ok, shift, kRadix - 1, s_cnt[wave], rank);
-        } else {
+    } else {
+        // park sorted run A in registers, sort run B, then merge by rank
+        uint32_t ak[kRunItems], ai[kRunItems];
 #pragma unroll
-            for (int q = 0; q < kSegRounds; q++) {
-                if (q < rounds) {
-                    uint32_t kk[1] = {k[q]}, rr[1];
-                    bool oo[1] = {ok[q]};
-                    wave_rank<uint32_t, 1>(kk, oo, shift, kRadix - 1, s_cnt[wave], rr);
-                    rank[q] = rr[0];
-                }
+        for (int q = 0; q < kRunItems; q++) {
+            ak[q] = sh.k[ca][t + q * kBlock];
+            ai[q] = sh.i[ca][t + q * kBlock];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kRunItems; q++) {
+            const uint32_t i = t + q * kBlock;
+            if (i < nb) {
+                sh.k[0][i] = bk[q];
+                sh.i[0][i] = kSegRun + i;
             }
         }
         __syncthreads();
-        const uint32_t tot = digit_wave_prefix(s_cnt);
-        uint32_t dummy;
-        s_start[t] = block_exclusive_scan(tot, s_wave, &dummy);
-        __syncthreads();
+        const int cb = lds_radix_sort(sh, nb, diff);
 #pragma unroll
-        for (int q = 0; q < kSegRounds; q++) {
-            if (ok[q]) {
-                const uint32_t dd = digit_of(k[q], shift, kRadix - 1);
-                const uint32_t pos = s_start[dd] + s_cnt[wave][dd] + rank[q];
-                s_k[cur ^ 1][pos] = k[q];
-                s_i[cur ^ 1][pos] = id[q];
-            }
+        for (int q = 0; q < kRunItems; q++) {
+            sh.k[cb ^ 1][t + q * kBlock] = ak[q];
+            sh.i[cb ^ 1][t + q * kBlock] = ai[q];
         }
         __syncthreads();
-        cur ^= 1;
+        // stable merge: an A item precedes every B item with an equal key (A indices are smaller)
+#pragma unroll
+        for (int q = 0; q < kRunItems; q++) {
+            const uint32_t i = t + q * kBlock;
+            fok[q] = true;
+            fk[q] = ak[q];
+            fi[q] = ai[q];
+            fp[q] = i + lds_rank(sh.k[cb], nb, ak[q], false);
+            const uint32_t j = i;
+            fok[kRunItems + q] = j < nb;
+            fk[kRunItems + q] = fok[kRunItems + q] ? sh.k[cb][j] : 0u;
+            fi[kRunItems + q] = fok[kRunItems + q] ? sh.i[cb][j] : 0u;
+            fp[kRunItems + q] = fok[kRunItems + q] ? j + lds_rank(sh.k[cb ^ 1], kSegRun, fk[kRunItems + q], true) : 0u;
+        }
     }
-    // exchange full keys (high half) and values by original index through the free buffer
+    // gather each item's high key half and value by its index in the segment (the segment is
+    // unmodified until every workgroup thread has gathered), then write in place
+    uint32_t hi[kSegItems], v[kSegItems];
 #pragma unroll
-    for (int q = 0; q < kSegRounds; q++) {
-        const uint32_t i = t + q * kBlock;
-        if (i < m) {
-            s_k[cur ^ 1][i] = (uint32_t)(kin[q] >> 32);
-            s_i[cur ^ 1][i] = vin[q];
+    for (int q = 0; q < kSegItems; q++) {
+        if (fok[q]) {
+            hi[q] = (uint32_t)(keys[begin + fi[q]] >> 32);
+            v[q] = vals[begin + fi[q]];
         }
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < kSegRounds; q++) {
-        const uint32_t i = t + q * kBlock;
-        if (i < m) {
-            const uint32_t src = s_i[cur][i];
-            keys[begin + i] = ((uint64_t)s_k[cur ^ 1][src] << 32) | s_k[cur][i];
-            vals[begin + i] = s_i[cur ^ 1][src];
+    for (int q = 0; q < kSegItems; q++) {
+        if (fok[q]) {
+            keys[begin + fp[q]] = ((uint64_t)hi[q] << 32) | fk[q];
+            vals[begin + fp[q]] = v[q];
         }
     }
 }

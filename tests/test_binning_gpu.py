@@ -54,6 +54,29 @@ def test_segmented_sort_small_and_oversized_tiles_bit_exact(K, T, hot):
     assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
 
 
+@pytest.mark.parametrize("distinct", [3, 1 << 20])
+def test_segmented_sort_run_merge_boundaries_bit_exact(distinct):
+    """Segments of exactly the sizes where the per-tile sort changes shape: one LDS run (<= 1024),
+    two runs merged by rank (1025..2048), the global fallback (> 2048).  With 3 distinct depth
+    values nearly every pair ties with pairs of the other run, so the merge's stability shows."""
+    sizes = [1, 2, 3, 63, 64, 65, 255, 256, 257, 1000, 1023, 1024, 1025, 1026, 1500, 2000, 2047, 2048, 2049, 2050,
+             3000, 4096, 4097, 9000]
+    sizes = sizes * 4  # 96 tiles, and enough pairs for the segmented path
+    T = 128
+    g = np.random.default_rng(distinct)
+    tiles = np.repeat(np.arange(len(sizes), dtype=np.uint64), sizes)
+    g.shuffle(tiles)
+    depth = g.integers(0, distinct, tiles.size).astype(np.uint64) * np.uint64(0x9E3779B1) & np.uint64(0xFFFFFFFF)
+    keys = (tiles << np.uint64(32)) | depth
+    vals = g.integers(0, 2**32, tiles.size, dtype=np.uint64).astype(np.uint32)
+    assert keys.size >= 65536
+    end = 32 + primitives.higher_msb(T)
+    ko, vo = primitives.sort_pairs(u64(keys), u32(vals), 0, end)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, end)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+
+
 @pytest.mark.parametrize("begin,end", [(0, 64), (8, 40), (3, 17), (0, 0), (60, 64), (0, 40), (0, 48), (0, 33)])
 def test_sort_u64_bit_ranges_and_stability(begin, end):
     g = np.random.default_rng(begin * 100 + end)

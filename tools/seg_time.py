@@ -1,0 +1,24 @@
+"""Per-kernel times of the binning sort (bench workload) with the library HIDEGS_LIB points at."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from hidegs_amd import _lib, primitives, synthetic  # noqa: E402
+
+wl = synthetic.binning_workload(2_000_000, 1920, 1080, seed=0, device="cuda")
+end = 32 + primitives.higher_msb(wl.num_tiles)
+for _ in range(10):
+    primitives.sort_pairs(wl.keys, wl.values, 0, end)
+torch.cuda.synchronize()
+with _lib.kernel_timer() as kt:
+    for _ in range(50):
+        primitives.sort_pairs(wl.keys, wl.values, 0, end)
+    torch.cuda.synchronize()
+    out = []
+    for nm in ("radix_scatter_u64", "segment_sort", "segment_sort_2k", "segment_sort_big", "segment_classify"):
+        ms, n = kt.get(nm)
+        if n:
+            out.append(f"{nm} {ms * 1e3 / n:.1f}us")
+print(os.environ.get("HIDEGS_LIB", "default"), " ".join(out), flush=True)
