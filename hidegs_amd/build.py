@@ -19,7 +19,7 @@ INCLUDE = os.path.join(HERE, "..", "include")
 OBJDIR = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libhidegs.so")
 SOURCES = ["abi.cpp", "timing.cpp", "primitives.hip", "knn.hip", "adam.hip"]
-HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(INCLUDE, "hidegs.h")]
+HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "block_scan.h"), os.path.join(INCLUDE, "hidegs.h")]
 
 # -ffp-contract=off: every fused multiply-add in the kernels is an explicit fmaf, so the
 # oracle (oracle/knn_ref.c) can reproduce each rounding step bit for bit.

@@ -22,6 +22,7 @@
 //    Stability is by construction: item order inside a wave is (round, lane),
 //    waves own consecutive 1024-item segments, tiles are ordered by the scan.
 // No kernel depends on dispatch order or XCD placement.
+#include "block_scan.h"
 #include "common.h"
 
 namespace hidegs {
@@ -37,32 +38,6 @@ constexpr int kRadix = 1 << kRadixBits;     // 256
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // ============================== scan ===========================================
-
-// Block-wide exclusive scan of one u32 per thread (256 threads); returns the
-// exclusive prefix and writes the block total to *total.
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t* total)
-{
-    const int lane = lane_id();
-    const int wave = threadIdx.x / kWave;
-    uint32_t inc = v;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t o = __shfl_up(inc, d, kWave);
-        if (lane >= d) inc += o;
-    }
-    if (lane == kWave - 1) s_wave[wave] = inc;
-    __syncthreads();
-    uint32_t woff = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kWavesPerBlock; w++) {
-        uint32_t s = s_wave[w];
-        if (w < wave) woff += s;
-        tot += s;
-    }
-    *total = tot;
-    __syncthreads();  // s_wave may be reused by the caller
-    return woff + inc - v;
-}
 
 // Loads one tile of u32 (striped 16-byte loads) and leaves it in LDS.
 __device__ __forceinline__ void load_tile_u32(const uint32_t* in, long long base, long long n,
@@ -99,34 +74,6 @@ __global__ __launch_bounds__(kBlock) void scan_reduce_kernel(const uint32_t* __r
     uint32_t total;
     block_exclusive_scan(sum, s_wave, &total);
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
-}
-
-// Exclusive scan of `count` u32 in place by ONE workgroup (count is small: tiles).
-__global__ __launch_bounds__(kBlock) void scan_small_kernel(uint32_t* __restrict__ data, int count,
-                                                            uint32_t* __restrict__ total_out)
-{
-    __shared__ uint32_t s_wave[kWavesPerBlock];
-    uint32_t carry = 0;
-    for (int base = 0; base < count; base += kTile) {
-        uint32_t v[kItems];
-        uint32_t sum = 0;
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-            int i = base + threadIdx.x * kItems + j;
-            v[j] = (i < count) ? data[i] : 0u;
-            sum += v[j];
-        }
-        uint32_t total;
-        uint32_t pre = block_exclusive_scan(sum, s_wave, &total) + carry;
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-            int i = base + threadIdx.x * kItems + j;
-            if (i < count) data[i] = pre;
-            pre += v[j];
-        }
-        carry += total;
-    }
-    if (total_out && threadIdx.x == 0) *total_out = carry;
 }
 
 // in and out may alias (in-place scan): each workgroup reads its whole tile before writing it.
