@@ -26,6 +26,14 @@ SZ = C.c_size_t
 # hidegs_alloc_fn: char* (*)(void* user, size_t nbytes)
 ALLOC_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_size_t)
 LL = C.c_longlong
+
+
+class AdamTensor(C.Structure):
+    """hidegs_adam_tensor (include/hidegs.h)."""
+    _fields_ = [("param", C.c_void_p), ("grad", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p),
+                ("relevant", C.c_void_p), ("rows", C.c_longlong), ("width", C.c_int), ("lr", C.c_double),
+                ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double), ("weight_decay", C.c_double),
+                ("step", C.c_longlong)]
 U32 = C.c_uint32
 
 # name -> (restype, argtypes); kept in the order of include/hidegs.h
@@ -57,6 +65,7 @@ SIGNATURES = {
     "hidegs_higher_msb": (U32, [U32]),
     "hidegs_masked_adam": (I, [P, P, P, P, P, LL, I, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                                 LL, P]),
+    "hidegs_masked_adam_multi": (I, [P, I, P]),
     "hidegs_kernel_timing": (None, [I]),
     "hidegs_kernel_timing_reset": (None, []),
     "hidegs_kernel_time": (I, [C.c_char_p, P, P]),

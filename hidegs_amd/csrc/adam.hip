@@ -1,4 +1,4 @@
-// adam.hip -- fused row-masked Adam step for one parameter tensor.
+// adam.hip -- fused row-masked Adam step for a list of parameter tensors.
 //
 // Replaces the per-parameter loop of the reference optimizer scene/OurAdam.py: the masked path
 // _single_tensor_adam (:249-337) gathers grad / exp_avg / exp_avg_sq / param rows with a
@@ -24,15 +24,42 @@
 // host as the reference computes them from step_t.item().
 #include <math.h>
 
+#include <string>
+
 #include "common.h"
 
 namespace hidegs {
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kQuadsPerThread = 2;                      // two 16-byte vectors per tensor in flight
+constexpr int kQuadsPerBlock = kBlock * kQuadsPerThread;  // 2048 elements per workgroup
+constexpr int kMaxTensors = 8;                          // tensors per launch
+
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 struct AdamScalars {
     float b1, a1, b2, a2, inv_bc2, eps, neg_step_size, wd;
+};
+
+struct AdamTensor {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    const unsigned char* relevant;
+    long long n;       // elements
+    int width;         // elements per row
+    int vec4;          // all four tensors 16-byte aligned
+    double inv_w;
+    AdamScalars s;
+};
+
+// One launch updates up to kMaxTensors parameters: workgroups [first[t], first[t+1]) own tensor t.
+struct AdamBatch {
+    int count;
+    int first[kMaxTensors + 1];
+    AdamTensor t[kMaxTensors];
 };
 
 __device__ __forceinline__ void adam_element(float& p, float g, float& m, float& v, const AdamScalars& s)
@@ -57,95 +84,193 @@ __device__ __forceinline__ long long row_of(long long e, int w, double inv_w)
     return r;
 }
 
-// Each thread owns 4 consecutive elements (one 16-byte vector when the tensors allow it).
-__global__ __launch_bounds__(kBlock) void masked_adam_kernel(float* __restrict__ param, const float* __restrict__ grad,
-                                                             float* __restrict__ exp_avg,
-                                                             float* __restrict__ exp_avg_sq,
-                                                             const unsigned char* __restrict__ relevant,
-                                                             long long n, int width, double inv_w, AdamScalars s,
-                                                             int vec4)
+// Which of the 4 elements from e0 lie in relevant rows (bit j = element e0 + j, e0 + j < n).
+__device__ __forceinline__ uint32_t relevant_bits(const AdamTensor& T, long long e0)
 {
-    const long long stride = (long long)gridDim.x * kBlock;
-    for (long long q = (long long)blockIdx.x * kBlock + threadIdx.x; 4 * q < n; q += stride) {
-        const long long e0 = 4 * q;
-        bool rel[4];
-        bool any = false;
+    uint32_t bits = 0;
+    if (T.relevant == nullptr) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const long long e = e0 + j;
-            rel[j] = e < n && (relevant == nullptr || relevant[row_of(e, width, inv_w)] != 0);
-            any |= rel[j];
+        for (int j = 0; j < 4; j++) bits |= (e0 + j < T.n ? 1u : 0u) << j;
+        return bits;
+    }
+    long long r = row_of(e0, T.width, T.inv_w);
+    long long c = e0 - r * T.width;
+    bool rel = T.relevant[r] != 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        if (j > 0 && ++c == T.width) {  // next row (width 1..3 can cross several rows in a quad)
+            c = 0;
+            r++;
+            if (e0 + j < T.n) rel = T.relevant[r] != 0;
         }
-        if (!any) continue;  // rows outside the mask: no traffic
-        if (vec4 && e0 + 4 <= n) {
-            float4 p = reinterpret_cast<float4*>(param)[q];
-            const float4 g = reinterpret_cast<const float4*>(grad)[q];
-            float4 m = reinterpret_cast<float4*>(exp_avg)[q];
-            float4 v = reinterpret_cast<float4*>(exp_avg_sq)[q];
-            float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
-            float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+        bits |= (e0 + j < T.n && rel ? 1u : 0u) << j;
+    }
+    return bits;
+}
+
+__device__ __forceinline__ f4 ld(const float* p, long long q) { return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p) + q); }
+__device__ __forceinline__ void st(float* p, long long q, f4 v) { __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p) + q); }
+
+__global__ __launch_bounds__(kBlock) void masked_adam_kernel(const AdamBatch batch)
+{
+    int ti = 0;
+    while (ti + 1 < batch.count && (int)blockIdx.x >= batch.first[ti + 1]) ti++;  // workgroup-uniform
+    const AdamTensor& T = batch.t[ti];
+    const long long q0 = (long long)(blockIdx.x - batch.first[ti]) * kQuadsPerBlock + threadIdx.x;
+    uint32_t bits[kQuadsPerThread];
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                if (rel[j]) adam_element(pp[j], gg[j], mm[j], vv[j], s);
-            reinterpret_cast<float4*>(param)[q] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-            reinterpret_cast<float4*>(exp_avg)[q] = make_float4(mm[0], mm[1], mm[2], mm[3]);
-            reinterpret_cast<float4*>(exp_avg_sq)[q] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-        } else {
+    for (int u = 0; u < kQuadsPerThread; u++) {
+        const long long q = q0 + u * kBlock;
+        bits[u] = 4 * q < T.n ? relevant_bits(T, 4 * q) : 0u;
+    }
+    if (T.vec4) {
+        f4 p[kQuadsPerThread], g[kQuadsPerThread], m[kQuadsPerThread], v[kQuadsPerThread];
 #pragma unroll
+        for (int u = 0; u < kQuadsPerThread; u++) {  // every load issued before any is used
+            const long long q = q0 + u * kBlock;
+            if (bits[u] && 4 * q + 4 <= T.n) {
+                p[u] = ld(T.param, q);
+                g[u] = ld(T.grad, q);
+                m[u] = ld(T.exp_avg, q);
+                v[u] = ld(T.exp_avg_sq, q);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kQuadsPerThread; u++) {
+            const long long q = q0 + u * kBlock;
+            if (bits[u] == 0) continue;  // rows outside the mask: no traffic
+            if (4 * q + 4 <= T.n) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (!(bits[u] >> j & 1u)) continue;
+                    float pp = p[u][j], mm = m[u][j], vv = v[u][j];
+                    adam_element(pp, g[u][j], mm, vv, T.s);
+                    p[u][j] = pp;
+                    m[u][j] = mm;
+                    v[u][j] = vv;
+                }
+                st(T.param, q, p[u]);
+                st(T.exp_avg, q, m[u]);
+                st(T.exp_avg_sq, q, v[u]);
+            } else {  // ragged end of the tensor
+                for (int j = 0; j < 4; j++) {
+                    if (!(bits[u] >> j & 1u)) continue;
+                    const long long e = 4 * q + j;
+                    float pp = T.param[e], mm = T.exp_avg[e], vv = T.exp_avg_sq[e];
+                    adam_element(pp, T.grad[e], mm, vv, T.s);
+                    T.param[e] = pp;
+                    T.exp_avg[e] = mm;
+                    T.exp_avg_sq[e] = vv;
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kQuadsPerThread; u++) {
+            const long long q = q0 + u * kBlock;
             for (int j = 0; j < 4; j++) {
-                if (!rel[j]) continue;
-                const long long e = e0 + j;
-                float p = param[e], m = exp_avg[e], v = exp_avg_sq[e];
-                adam_element(p, grad[e], m, v, s);
-                param[e] = p;
-                exp_avg[e] = m;
-                exp_avg_sq[e] = v;
+                if (!(bits[u] >> j & 1u)) continue;
+                const long long e = 4 * q + j;
+                float pp = T.param[e], mm = T.exp_avg[e], vv = T.exp_avg_sq[e];
+                adam_element(pp, T.grad[e], mm, vv, T.s);
+                T.param[e] = pp;
+                T.exp_avg[e] = mm;
+                T.exp_avg_sq[e] = vv;
             }
         }
     }
 }
 
+int check_tensor(const hidegs_adam_tensor& a, int i)
+{
+    const std::string who = "masked_adam: tensor " + std::to_string(i);
+    if (a.rows < 0 || a.width <= 0) return fail(HIDEGS_E_ARG, who + ": bad shape");
+    if (a.step < 1) return fail(HIDEGS_E_ARG, who + ": step counts from 1 (after the increment)");
+    if (a.rows * (long long)a.width > 0 && (!a.param || !a.grad || !a.exp_avg || !a.exp_avg_sq))
+        return fail(HIDEGS_E_ARG, who + ": NULL tensor");
+    return 0;
+}
+
+AdamTensor describe(const hidegs_adam_tensor& a)
+{
+    AdamTensor T;
+    T.param = a.param;
+    T.grad = a.grad;
+    T.exp_avg = a.exp_avg;
+    T.exp_avg_sq = a.exp_avg_sq;
+    T.relevant = a.relevant;
+    T.n = a.rows * (long long)a.width;
+    T.width = a.width;
+    T.inv_w = 1.0 / (double)a.width;
+    T.vec4 = ((reinterpret_cast<uintptr_t>(a.param) | reinterpret_cast<uintptr_t>(a.grad) |
+               reinterpret_cast<uintptr_t>(a.exp_avg) | reinterpret_cast<uintptr_t>(a.exp_avg_sq)) & 15) == 0;
+    // scalars exactly as the reference forms them (OurAdam.py:305-325), in double, cast once
+    const double bias_correction1 = 1.0 - pow(a.beta1, (double)a.step);
+    const double bias_correction2 = 1.0 - pow(a.beta2, (double)a.step);
+    const double step_size = a.lr / bias_correction1;
+    const double bc2_sqrt = sqrt(bias_correction2);
+    T.s.b1 = (float)a.beta1;
+    T.s.a1 = (float)(1.0 - a.beta1);
+    T.s.b2 = (float)a.beta2;
+    T.s.a2 = (float)(1.0 - a.beta2);
+    T.s.inv_bc2 = (float)(1.0 / bc2_sqrt);  // reciprocal in double, rounded once (torch probe)
+    T.s.eps = (float)a.eps;
+    T.s.neg_step_size = (float)(-step_size);
+    T.s.wd = (float)a.weight_decay;
+    return T;
+}
+
 }  // namespace
 
-int masked_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const unsigned char* relevant,
-                long long rows, int width, double lr, double beta1, double beta2, double eps, double weight_decay,
-                long long step, hipStream_t stream)
+int masked_adam_multi(const hidegs_adam_tensor* tensors, int count, hipStream_t stream)
 {
-    if (rows < 0 || width <= 0) return fail(HIDEGS_E_ARG, "masked_adam: bad shape");
-    if (step < 1) return fail(HIDEGS_E_ARG, "masked_adam: step counts from 1 (after the increment)");
-    const long long n = rows * (long long)width;
-    if (n == 0) return 0;
-    if (!param || !grad || !exp_avg || !exp_avg_sq) return fail(HIDEGS_E_ARG, "masked_adam: NULL tensor");
-    // scalars exactly as the reference forms them (OurAdam.py:305-325), in double, cast once
-    const double bias_correction1 = 1.0 - pow(beta1, (double)step);
-    const double bias_correction2 = 1.0 - pow(beta2, (double)step);
-    const double step_size = lr / bias_correction1;
-    const double bc2_sqrt = sqrt(bias_correction2);
-    AdamScalars s;
-    s.b1 = (float)beta1;
-    s.a1 = (float)(1.0 - beta1);
-    s.b2 = (float)beta2;
-    s.a2 = (float)(1.0 - beta2);
-    s.inv_bc2 = (float)(1.0 / bc2_sqrt);  // reciprocal in double, rounded once (torch probe)
-    s.eps = (float)eps;
-    s.neg_step_size = (float)(-step_size);
-    s.wd = (float)weight_decay;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
-                           reinterpret_cast<uintptr_t>(exp_avg) | reinterpret_cast<uintptr_t>(exp_avg_sq)) & 15) == 0;
-    const long long quads = (n + 3) / 4;
-    const long long want = (quads + kBlock - 1) / kBlock;
-    const int grid = (int)(want < 8192 ? want : 8192);
-    HIDEGS_LAUNCH("masked_adam", masked_adam_kernel, dim3(grid), dim3(kBlock), 0, stream, param, grad, exp_avg,
-                  exp_avg_sq, relevant, n, width, 1.0 / (double)width, s, aligned ? 1 : 0);
+    if (count < 0 || (count > 0 && !tensors)) return fail(HIDEGS_E_ARG, "masked_adam: bad tensor list");
+    for (int i = 0; i < count; i++)
+        if (int rc = check_tensor(tensors[i], i)) return rc;
+    for (int i0 = 0; i0 < count; i0 += kMaxTensors) {  // kMaxTensors per launch
+        AdamBatch batch;
+        batch.count = 0;
+        long long blocks = 0;
+        for (int i = i0; i < count && i < i0 + kMaxTensors; i++) {
+            const AdamTensor T = describe(tensors[i]);
+            if (T.n == 0) continue;
+            const long long quads = (T.n + 3) / 4;
+            batch.first[batch.count] = (int)blocks;
+            batch.t[batch.count++] = T;
+            blocks += (quads + kQuadsPerBlock - 1) / kQuadsPerBlock;
+            if (blocks > 0x7fffffffLL) return fail(HIDEGS_E_ARG, "masked_adam: tensors too large for one launch");
+        }
+        if (batch.count == 0) continue;
+        batch.first[batch.count] = (int)blocks;
+        HIDEGS_LAUNCH("masked_adam", masked_adam_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, batch);
+    }
     return check_launch("masked_adam", stream, 0);
 }
 
 }  // namespace hidegs
 
+extern "C" int hidegs_masked_adam_multi(const hidegs_adam_tensor* tensors, int count, void* stream)
+{
+    return hidegs::masked_adam_multi(tensors, count, hidegs::as_stream(stream));
+}
+
 extern "C" int hidegs_masked_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                                   const unsigned char* relevant, long long rows, int width, double lr, double beta1,
                                   double beta2, double eps, double weight_decay, long long step, void* stream)
 {
-    return hidegs::masked_adam(param, grad, exp_avg, exp_avg_sq, relevant, rows, width, lr, beta1, beta2, eps,
-                               weight_decay, step, hidegs::as_stream(stream));
+    hidegs_adam_tensor t;
+    t.param = param;
+    t.grad = grad;
+    t.exp_avg = exp_avg;
+    t.exp_avg_sq = exp_avg_sq;
+    t.relevant = relevant;
+    t.rows = rows;
+    t.width = width;
+    t.lr = lr;
+    t.beta1 = beta1;
+    t.beta2 = beta2;
+    t.eps = eps;
+    t.weight_decay = weight_decay;
+    t.step = step;
+    return hidegs::masked_adam_multi(&t, 1, hidegs::as_stream(stream));
 }

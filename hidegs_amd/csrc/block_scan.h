@@ -17,12 +17,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
 {
     const int lane = lane_id();
     const int wave = threadIdx.x / kWave;
-    uint32_t inc = v;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t o = __shfl_up(inc, d, kWave);
-        if (lane >= d) inc += o;
-    }
+    const uint32_t inc = wave_inclusive_scan_u32(v);
     if (lane == kWave - 1) s_wave[wave] = inc;
     __syncthreads();
     uint32_t woff = 0, tot = 0;

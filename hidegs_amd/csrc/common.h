@@ -56,6 +56,28 @@ __device__ __forceinline__ T wave_shfl_xor(T v, int m)
     return __shfl_xor(v, m, kWave);
 }
 
+// Inclusive prefix sum over the 64 lanes with DPP moves (row_shr within rows of 16, then the
+// row_bcast:15 / row_bcast:31 carries of GFX9): VALU-latency steps instead of LDS-path shuffles.
+// Every lane of the wave must be active.
+__device__ __forceinline__ uint32_t wave_inclusive_scan_u32(uint32_t v)
+{
+    const int lane = lane_id(), rl = lane & 15;
+    int x = (int)v, t;
+    t = __builtin_amdgcn_mov_dpp(x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    if (rl >= 1) x += t;
+    t = __builtin_amdgcn_mov_dpp(x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    if (rl >= 2) x += t;
+    t = __builtin_amdgcn_mov_dpp(x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    if (rl >= 4) x += t;
+    t = __builtin_amdgcn_mov_dpp(x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    if (rl >= 8) x += t;
+    t = __builtin_amdgcn_mov_dpp(x, 0x142, 0xf, 0xf, false);  // row_bcast:15
+    if ((lane & 31) >= 16) x += t;
+    t = __builtin_amdgcn_mov_dpp(x, 0x143, 0xf, 0xf, false);  // row_bcast:31
+    if (lane >= 32) x += t;
+    return (uint32_t)x;
+}
+
 __device__ __forceinline__ float wave_max(float v)
 {
 #pragma unroll

@@ -124,29 +124,32 @@ __device__ __forceinline__ uint32_t digit_of(K key, int shift, uint32_t mask)
 // Stable wave64 ranking of R rounds of items (round r, lane l = the wave's item r*64 + l,
 // in input order).  cnt = this wave's 256 digit counters, zero on entry; on exit cnt[d] is
 // the number of valid items with digit d and rank[r] the item's position among them.
-// The lanes sharing a digit are found with kRadixBits ballots; the lowest such lane bumps
-// the counter (LDS ops of one wave retire in order, so the read precedes the write).
+// The lanes sharing a digit are found with one ballot per digit bit; bits outside `vary`
+// are equal in every item (a caller's guarantee) and need none.  The lowest lane of each
+// digit group bumps the counter (LDS ops of one wave retire in order, so the read precedes
+// the write).
 template <typename K, int R>
 __device__ __forceinline__ void wave_rank(const K (&k)[R], const bool (&ok)[R], int shift, uint32_t mask,
-                                          uint32_t* cnt, uint32_t (&rank)[R])
+                                          uint32_t* cnt, uint32_t (&rank)[R], uint32_t vary)
 {
-    const int lane = lane_id();
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const uint32_t d = digit_of(k[r], shift, mask);
-        uint64_t m = __ballot(ok[r]);
+        const uint64_t okb = __ballot(ok[r]);
+        uint32_t mlo = (uint32_t)okb, mhi = (uint32_t)(okb >> 32);  // lanes with the same digit
 #pragma unroll
         for (int b = 0; b < kRadixBits; b++) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            m &= bit ? bb : ~bb;
+            if (!((vary >> b) & 1u)) continue;  // wave-uniform
+            const uint32_t nb = ((d >> b) & 1u) - 1u;  // 0 when the bit is set, ~0 when clear
+            const uint64_t bb = __ballot(nb == 0u);
+            mlo &= nb ^ (uint32_t)bb;
+            mhi &= nb ^ (uint32_t)(bb >> 32);
         }
-        const uint32_t below = (uint32_t)__popcll(m & lt);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
         uint32_t old = 0;
         if (ok[r]) old = cnt[d];
         __builtin_amdgcn_wave_barrier();
-        if (ok[r] && below == 0) cnt[d] = old + (uint32_t)__popcll(m);
+        if (ok[r] && below == 0) cnt[d] = old + (uint32_t)(__popc(mlo) + __popc(mhi));
         __builtin_amdgcn_wave_barrier();
         rank[r] = old + below;
     }
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
     }
     __syncthreads();
     uint32_t rank[kItems];
-    wave_rank<K, kItems>(k, ok, shift, mask, s_cnt[wave], rank);
+    wave_rank<K, kItems>(k, ok, shift, mask, s_cnt[wave], rank, mask);
     __syncthreads();
 
     const int d = t;
@@ -340,7 +343,8 @@ __device__ __forceinline__ int lds_radix_sort(SegShared& sh, const uint32_t n, c
     const uint32_t w0 = wave * C;
     int cur = 0;
     for (int shift = 0; shift < HIDEGS_SEG_BITS; shift += kRadixBits) {
-        if (((diff >> shift) & (kRadix - 1)) == 0) continue;  // block-uniform
+        const uint32_t vary = (diff >> shift) & (kRadix - 1);
+        if (vary == 0) continue;  // digit constant over the segment (block-uniform)
         for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&sh.cnt[0][0])[i] = 0;
         __syncthreads();
         uint32_t k[kRunItems], id[kRunItems], rank[kRunItems];
@@ -353,14 +357,14 @@ __device__ __forceinline__ int lds_radix_sort(SegShared& sh, const uint32_t n, c
             id[q] = ok[q] ? sh.i[cur][i] : 0u;
         }
         if (rounds == kRunItems) {
-            wave_rank<uint32_t, kRunItems>(k, ok, shift, kRadix - 1, sh.cnt[wave], rank);
+            wave_rank<uint32_t, kRunItems>(k, ok, shift, kRadix - 1, sh.cnt[wave], rank, vary);
         } else {  // rounds past `rounds` hold no item: skip their ranking (block-uniform)
 #pragma unroll
             for (int q = 0; q < kRunItems; q++) {
                 if (q < rounds) {
                     uint32_t kk[1] = {k[q]}, rr[1];
                     bool oo[1] = {ok[q]};
-                    wave_rank<uint32_t, 1>(kk, oo, shift, kRadix - 1, sh.cnt[wave], rr);
+                    wave_rank<uint32_t, 1>(kk, oo, shift, kRadix - 1, sh.cnt[wave], rr, vary);
                     rank[q] = rr[0];
                 }
             }
@@ -583,7 +587,7 @@ __global__ __launch_bounds__(kBlock) void segment_sort_big_kernel(uint64_t* __re
                     k[q] = ok[q] ? sk[begin + i] : 0ull;
                     v[q] = ok[q] ? sv[begin + i] : 0u;
                 }
-                wave_rank<uint64_t, kItems>(k, ok, shift, kRadix - 1, s_cnt[wave], rank);
+                wave_rank<uint64_t, kItems>(k, ok, shift, kRadix - 1, s_cnt[wave], rank, kRadix - 1);
                 __syncthreads();
                 const uint32_t tot = digit_wave_prefix(s_cnt);
                 __syncthreads();

@@ -7,9 +7,9 @@ keep their parameter and moments unchanged; an empty `relevant` updates every ro
 (OurAdam.py:230-244).  Each parameter's step counter advances on every call, masked or not,
 exactly as the reference's `step_t += 1`.
 
-Each parameter is updated by one fused gfx950 kernel (hidegs_masked_adam, csrc/adam.hip)
-that reads and writes every relevant element once, instead of the reference's boolean-index
-gathers, eight elementwise ops and scatters.  Results equal the reference's torch ops on the
+The whole step is one fused gfx950 launch over all parameters (hidegs_masked_adam_multi,
+csrc/adam.hip) that reads and writes every relevant element once, instead of the reference's
+per-parameter boolean-index gathers, eight elementwise ops and scatters.  Results equal the reference's torch ops on the
 GPU bit for bit (tests/test_adam_gpu.py).  No CPU fallback: parameters must live on the GPU.
 
 Not supported, as in the reference's masked path, which fails on them with a shape error:
@@ -60,7 +60,8 @@ class Adam(Optimizer):
                 loss = closure()
         dense = relevant.size(0) == 0
         masks = {}
-        L = _lib.lib()
+        batches = {}  # device -> tensor descriptors, one native call per device
+        keep = []     # tensors referenced by the descriptors stay alive until the call returns
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
             for p in group["params"]:
@@ -87,10 +88,15 @@ class Adam(Optimizer):
                 for t in (p, p.grad, state["exp_avg"], state["exp_avg_sq"]):
                     if not t.is_contiguous() or t.dtype != torch.float32:
                         raise RuntimeError("masked Adam needs contiguous float32 parameters, grads and moments")
-                with torch.cuda.device(dev):
-                    rc = L.hidegs_masked_adam(_lib.ptr(p), _lib.ptr(p.grad), _lib.ptr(state["exp_avg"]),
-                                              _lib.ptr(state["exp_avg_sq"]), _lib.ptr(mask), rows, width,
-                                              float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
-                                              float(group["weight_decay"]), step, _lib.stream_handle(dev))
-                    _lib.check(rc, "masked Adam")
+                keep.append((p, p.grad, state["exp_avg"], state["exp_avg_sq"], mask))
+                batches.setdefault(dev, []).append(_lib.AdamTensor(
+                    _lib.ptr(p), _lib.ptr(p.grad), _lib.ptr(state["exp_avg"]), _lib.ptr(state["exp_avg_sq"]),
+                    _lib.ptr(mask), rows, width, float(group["lr"]), float(beta1), float(beta2),
+                    float(group["eps"]), float(group["weight_decay"]), step))
+        L = _lib.lib()
+        for dev, descs in batches.items():
+            arr = (_lib.AdamTensor * len(descs))(*descs)
+            with torch.cuda.device(dev):
+                _lib.check(L.hidegs_masked_adam_multi(arr, len(descs), _lib.stream_handle(dev)), "masked Adam")
+        del keep
         return loss

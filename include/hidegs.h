@@ -24,6 +24,7 @@
  *   hidegs_higher_msb           <- getHigherMsb (HR/cuda_rasterizer/rasterizer_impl.cu:35-50)
  *   hidegs_masked_adam          <- the per-parameter update of scene/OurAdam.py (_single_tensor_adam :249-337,
  *                                  _single_tensor_adam2 :340-420)
+ *   hidegs_masked_adam_multi    <- the loop over parameters of Adam.step(relevant) (scene/OurAdam.py:106-175)
  * INTEGRATION.md shows the Python-side bindings.
  */
 #ifndef HIDEGS_H_INCLUDED
@@ -145,13 +146,34 @@ uint32_t hidegs_higher_msb(uint32_t n);
  * Fused row-masked Adam step on one fp32 parameter of rows x width values (row-major).  Rows
  * with relevant[r] != 0 -- every row when relevant is NULL (the reference's empty-mask path) --
  * are updated exactly as OurAdam's torch ops update them on this GPU (op order and rounding in
- * hidegs_amd/csrc/adam.hip); other rows are neither read nor written.  `step` is the
+ * hidegs_amd/csrc/adam.hip); other rows keep their bits (a 16-byte vector that straddles a relevant
+ * row is rewritten unchanged; rows without a relevant element are not accessed).  `step` is the
  * parameter's step count after this call's increment (>= 1); lr, betas, eps, weight_decay are
  * the Python doubles the reference passes.  param, exp_avg, exp_avg_sq are updated in place.
  */
 int hidegs_masked_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                        const unsigned char* relevant, long long rows, int width, double lr, double beta1,
                        double beta2, double eps, double weight_decay, long long step, void* stream);
+
+/* One parameter of a multi-tensor masked Adam step (the fields of hidegs_masked_adam). */
+typedef struct hidegs_adam_tensor {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    const unsigned char* relevant; /* rows bytes; NULL = every row */
+    long long rows;
+    int width;
+    double lr, beta1, beta2, eps, weight_decay;
+    long long step;
+} hidegs_adam_tensor;
+
+/*
+ * The whole optimizer step of OurAdam.step(relevant) (scene/OurAdam.py:106-175): every listed
+ * parameter updated as hidegs_masked_adam would, with its own hyper-parameters and step count,
+ * in one launch per 8 tensors.  `tensors` is a host array of `count` descriptors.
+ */
+int hidegs_masked_adam_multi(const hidegs_adam_tensor* tensors, int count, void* stream);
 
 /*
  * [host] Per-kernel device timing.  While enabled, every kernel this library launches is

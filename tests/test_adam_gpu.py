@@ -135,3 +135,43 @@ def test_unaligned_views_take_the_scalar_path():
     st = {"a": {"step": torch.tensor(0.), "exp_avg": torch.zeros_like(ref), "exp_avg_sq": torch.zeros_like(ref)}}
     torch_reference_step({"a": ref}, {"a": p.grad}, st, torch.zeros(0, dtype=torch.bool), {"a": 0.01}, eps=1e-8)
     assert torch.equal(p.detach(), ref)
+
+
+def test_multi_tensor_launch_batches_widths_and_ragged_ends(oracle_lib):
+    """hidegs_masked_adam_multi over 11 tensors (more than one launch's 8), widths 1..45, row counts
+    that leave ragged 16-byte vectors, each with its own mask (or none), lr, weight decay and step
+    count -- every tensor bit-exact against the oracle."""
+    g = torch.Generator().manual_seed(21)
+    specs = [(1, 1), (2, 5), (3, 7), (4, 4099), (5, 333), (6, 1), (7, 2048), (1, 65537), (3, 12345), (45, 1001),
+             (2, 3)]
+    dev = torch.device("cuda", 0)
+    descs, keep, expect = [], [], []
+    for i, (w, r) in enumerate(specs):
+        p = torch.randn(r, w, generator=g)
+        gr = torch.randn(r, w, generator=g)
+        m = torch.randn(r, w, generator=g).abs() * 0.1
+        v = torch.rand(r, w, generator=g) * 0.01
+        rel = None if i % 3 == 0 else (torch.rand(r, generator=g) < 0.5)
+        lr, wd, step = 0.001 * (i + 1), (0.01 if i % 4 == 1 else 0.0), 1 + i % 3
+        pe, me, ve = p.numpy().copy(), m.numpy().copy(), v.numpy().copy()
+        oracle.masked_adam(pe, gr.numpy().copy(), me, ve, None if rel is None else rel.numpy(), lr, 0.9, 0.999,
+                           1e-15, wd, step)
+        expect.append((pe, me, ve))
+        t = [x.to(dev) for x in (p, gr, m, v)] + [None if rel is None else rel.to(dev)]
+        keep.append(t)
+        descs.append(_lib.AdamTensor(*[_lib.ptr(x) for x in t], r, w, lr, 0.9, 0.999, 1e-15, wd, step))
+    arr = (_lib.AdamTensor * len(descs))(*descs)
+    _lib.check(_lib.lib().hidegs_masked_adam_multi(arr, len(descs), _lib.stream_handle(dev)), "multi")
+    torch.cuda.synchronize()
+    for (pe, me, ve), t, spec in zip(expect, keep, specs):
+        for got, exp in ((t[0], pe), (t[2], me), (t[3], ve)):
+            assert np.array_equal(got.cpu().numpy().view(np.uint32), exp.view(np.uint32)), spec
+
+
+def test_multi_tensor_rejects_bad_descriptor():
+    dev = torch.device("cuda", 0)
+    x = torch.zeros(4, 4, device=dev)
+    bad = _lib.AdamTensor(_lib.ptr(x), _lib.ptr(x), _lib.ptr(x), _lib.ptr(x), None, 4, 4, 0.1, 0.9, 0.999, 1e-8, 0.0, 0)
+    arr = (_lib.AdamTensor * 1)(bad)
+    with pytest.raises(RuntimeError, match="step counts from 1"):
+        _lib.check(_lib.lib().hidegs_masked_adam_multi(arr, 1, _lib.stream_handle(dev)), "multi")
