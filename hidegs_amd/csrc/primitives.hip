@@ -697,21 +697,27 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
 
     const K* src_k = keys_in;
     const uint32_t* src_v = vals_in;
+    // balanced digit widths (13 tile bits: 7 + 6, not 8 + 5): fewer buckets per pass mean
+    // longer runs per bucket in each tile's scatter, i.e. fuller write lines
+    const int span = end_bit - lo_bit;
+    int shift = lo_bit;
     for (int p = 0; p < lsd_passes; p++) {
-        const int shift = lo_bit + p * kRadixBits;
-        const int bits = (end_bit - shift) < kRadixBits ? (end_bit - shift) : kRadixBits;
+        const int bits = (span * (p + 1)) / lsd_passes - (span * p) / lsd_passes;
         const uint32_t mask = (1u << bits) - 1u;
         const bool to_out = ((lsd_passes - 1 - p) % 2) == 0;
         K* dk = to_out ? keys_out : alt_k;
         uint32_t* dv = to_out ? vals_out : alt_v;
         HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_hist_u64" : "radix_hist_u32"), radix_hist_kernel<K>, dim3(nt),
                       dim3(kBlock), 0, stream, src_k, n, shift, mask, nt, counts);
-        HIDEGS_LAUNCH("radix_digit_scan", radix_digit_scan_kernel, dim3(kRadix), dim3(kBlock), 0, stream, counts, nt,
-                      totals);
+        // digits above `mask` never occur: their (stale) totals only follow the used digits in the
+        // scatter's exclusive scan, and their counts are never read
+        HIDEGS_LAUNCH("radix_digit_scan", radix_digit_scan_kernel, dim3(mask + 1), dim3(kBlock), 0, stream, counts,
+                      nt, totals);
         HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"), radix_scatter_kernel<K>,
                       dim3(nt), dim3(kBlock), 0, stream, src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals);
         src_k = dk;
         src_v = dv;
+        shift += bits;
     }
     if (segmented) {
         const int nseg = 1 << (end_bit - 32);
