@@ -86,14 +86,18 @@ __device__ __forceinline__ float box_box_lb(const Box& b, float4 qlo, float4 qhi
 }
 
 // Keep the three smallest values seen (a multiset, as updateKBest<3> does).  NaN never enters.
+// Every value here is a non-negative float (a sum of squares, FLT_MAX or +inf), whose bit
+// patterns order like unsigned integers: the min/max network runs on the bits, which spares the
+// NaN-quieting canonicalisation that fminf/fmaxf of loop-carried values costs on gfx950.
 __device__ __forceinline__ void kbest(float d, float& b0, float& b1, float& b2)
 {
-    d = (d == d) ? d : FLT_MAX;
-    const float t0 = fminf(b0, d), u0 = fmaxf(b0, d);
-    const float t1 = fminf(b1, u0), u1 = fmaxf(b1, u0);
-    b2 = fminf(b2, u1);
-    b1 = t1;
-    b0 = t0;
+    const uint32_t x = (d == d) ? __float_as_uint(d) : __float_as_uint(FLT_MAX);
+    const uint32_t c0 = __float_as_uint(b0), c1 = __float_as_uint(b1), c2 = __float_as_uint(b2);
+    const uint32_t t0 = min(c0, x), u0 = max(c0, x);
+    const uint32_t t1 = min(c1, u0), u1 = max(c1, u0);
+    b2 = __uint_as_float(min(c2, u1));
+    b1 = __uint_as_float(t1);
+    b0 = __uint_as_float(t0);
 }
 
 // Value of lane `src` as a wave-uniform (scalar-register) float.
@@ -315,8 +319,21 @@ constexpr int kGroups = 4;                  // query groups per wave for the coa
 constexpr int kSuperBatch = 4;              // super-boxes tested per lane per batch
 constexpr int kLeafBatch = 4;               // passing super-boxes whose leaf boxes load together
 constexpr int kListCap = 256;               // candidate leaves buffered per wave
-constexpr int kFlushBatch = 4;              // candidate leaves loaded together
+#ifndef HIDEGS_KNN_FLUSH_BATCH
+#define HIDEGS_KNN_FLUSH_BATCH 4
+#endif
+constexpr int kFlushBatch = HIDEGS_KNN_FLUSH_BATCH;  // candidate leaves loaded together
 constexpr int kGroupLanes = kWave / kGroups;
+#ifndef HIDEGS_KNN_BAILOUT
+#define HIDEGS_KNN_BAILOUT 256
+#endif
+constexpr int kBailout = HIDEGS_KNN_BAILOUT;  // candidate leaves after which a wave hands its queries to phase 2
+#ifndef HIDEGS_KNN_SEED_NEIGHBORS
+#define HIDEGS_KNN_SEED_NEIGHBORS 1  // 0: seed from the own leaf only (A/B builds)
+#endif
+#ifndef HIDEGS_KNN_POINT_FILTER
+#define HIDEGS_KNN_POINT_FILTER 1  // 0: evaluate whole passing sub-boxes (A/B builds, tools/build_variant.py)
+#endif
 
 // Boxes of the active queries of each group of kGroupLanes lanes, broadcast to every lane.
 __device__ __forceinline__ void group_boxes(float4 p, bool active, float4 (&lo)[kGroups], float4 (&hi)[kGroups])
@@ -378,10 +395,22 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
     const float4 p = valid ? sp[me] : make_float4(0.f, 0.f, 0.f, 0.f);
     float b0 = FLT_MAX, b1 = FLT_MAX, b2 = FLT_MAX;
 
-    // seed from the own leaf
+    // seed from the own leaf and, with HIDEGS_KNN_SEED_NEIGHBORS, its two Morton neighbours (a query
+    // near its leaf's border finds a tight bound there, which prunes the box walk below)
     {
         const int nc = min(kLeaf, P - L * kLeaf);
         for (int k0 = 0; k0 < nc; k0 += kChunk) eval_lanes(p, k0, nc, lane, p, b0, b1, b2);
+#if HIDEGS_KNN_SEED_NEIGHBORS
+        const int ln = L - 1, rn = L + 1;
+        const float4 pl = ln >= 0 ? sp[ln * kLeaf + lane] : p;
+        const float4 pr = rn < nleaves ? sp[min(rn * kLeaf + lane, P - 1)] : p;
+        if (ln >= 0)
+            for (int k0 = 0; k0 < kLeaf; k0 += kChunk) eval_lanes(pl, k0, kLeaf, -1, p, b0, b1, b2);
+        if (rn < nleaves) {
+            const int nr = min(kLeaf, P - rn * kLeaf);
+            for (int k0 = 0; k0 < nr; k0 += kChunk) eval_lanes(pr, k0, nr, -1, p, b0, b1, b2);
+        }
+#endif
     }
 
     // outliers -> phase 2
@@ -420,6 +449,8 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
         group_bounds(b2, active, gub);
         uint32_t* list = s_list[wave];
         int nnear = 0, nfar = 0;  // list[0, nnear) near leaves, list[cap - nfar, cap) far leaves
+        int listed = 0;           // candidate leaves so far
+        bool bail = false;
         uint32_t n_coarse = 0, n_fine = 0;
 
         // evaluate and empty the candidate list
@@ -454,13 +485,37 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
                         if (__ballot(active && box_point_lb(sb, p) <= b2)) smask4 |= 1u << j;
                     }
                     const int nc = min(kLeaf, P - Cb[q] * kLeaf);
+#if HIDEGS_KNN_POINT_FILTER
+                    // point-level filter: lane c holds point c of the leaf; it is evaluated only if
+                    // its sub-box passed some lane's own bound AND it lies within some query group's
+                    // bound of that group's box (both skip only points that cannot improve any
+                    // active query's three best)
+                    uint64_t sm = 0;
+#pragma unroll
+                    for (int j = 0; j < kSub; j++)
+                        if (smask4 >> j & 1u) sm |= 0xFFFFull << (kChunk * j);
+                    bool usable = false;
+#pragma unroll
+                    for (int g = 0; g < kGroups; g++) usable |= box_point_lb(Box{glo[g], ghi[g]}, pt[q]) <= gub[g];
+                    uint64_t pm = __ballot(usable && lane < nc) & sm;
+                    n_fine += (uint32_t)__popcll(pm);
+                    while (pm) {
+                        const int k = __builtin_ctzll(pm);
+                        pm &= pm - 1;
+                        const float4 c = make_float4(uniform_lane(pt[q].x, k), uniform_lane(pt[q].y, k),
+                                                     uniform_lane(pt[q].z, k), 0.f);
+                        kbest(sqdist(p, c), b0, b1, b2);
+                    }
+#else
                     while (smask4) {
                         const int j = __builtin_ctz(smask4);
                         smask4 &= smask4 - 1;
                         n_fine++;
                         eval_lanes(pt[q], j * kChunk, nc, -1, p, b0, b1, b2);
                     }
+#endif
                 }
+                group_bounds(b2, active, gub);  // tighter group bounds for the next batch
             }
             nnear = nfar = 0;
             group_bounds(b2, active, gub);
@@ -511,7 +566,7 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
                     if (q >= ns) break;
                     const int l = S[q] * kFan + lane;
                     bool lpass = false, near = false;
-                    if (l < nleaves && l != L) {
+                    if (l < nleaves && l != L && (!HIDEGS_KNN_SEED_NEIGHBORS || (l != L - 1 && l != L + 1))) {
 #pragma unroll
                         for (int g = 0; g < kGroups; g++) {
                             const float d = box_box_lb(lb[q], glo[g], ghi[g]);
@@ -522,6 +577,11 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
                     const uint64_t lm = __ballot(lpass);
                     const int cnt = __popcll(lm);
                     if (cnt == 0) continue;
+                    listed += cnt;
+                    if (listed > kBailout) {  // a long-tail wave: its queries go to phase 2
+                        bail = true;
+                        break;
+                    }
                     if (nnear + nfar + cnt > kListCap) flush();
                     // leaves touching a query group's box go to the front and are evaluated first,
                     // so the bounds shrink before the farther leaves are filtered
@@ -533,9 +593,24 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
                     nfar += __popcll(fm);
                     __builtin_amdgcn_wave_barrier();
                 }
+                if (bail) break;
             }
+            if (bail) break;
         }
-        if (nnear + nfar) flush();
+        if (bail) {
+            // Waves whose coarse walk passes more than kBailout leaves (queries at the edge of a
+            // sparse region inflate their group's bound) would run for milliseconds while the rest
+            // of the grid idles; phase 2 searches each of their queries with its own bound instead.
+            const uint64_t am = __ballot(active);
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&counters->hard, (uint32_t)__popcll(am));
+            base = __shfl(base, 0, kWave);
+            const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+            if (active) hard[base + __popcll(am & lt)] = (uint32_t)me;
+            active = false;
+        } else if (nnear + nfar) {
+            flush();
+        }
         if (stats && lane == 0) {  // diagnostics only (HIDEGS_KNN_STATS): same-address atomics are slow
             atomicAdd(&counters->coarse, (unsigned long long)n_coarse);
             atomicAdd(&counters->fine, (unsigned long long)n_fine);

@@ -29,7 +29,10 @@ namespace hidegs {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kItems = 16;
+#ifndef HIDEGS_RADIX_ITEMS
+#define HIDEGS_RADIX_ITEMS 16  // items per thread of a scan / radix tile (experiments: tools/build_variant.py)
+#endif
+constexpr int kItems = HIDEGS_RADIX_ITEMS;
 constexpr int kTile = kBlock * kItems;       // 4096
 constexpr int kWavesPerBlock = kBlock / kWave;  // 4
 constexpr int kRadixBits = 8;
@@ -230,7 +233,8 @@ __global__ __launch_bounds__(kBlock) void radix_digit_scan_kernel(uint32_t* __re
     if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
-// Stable scatter of one tile.  LDS: keys + values of the tile, per-wave digit counters.
+// Stable scatter of one tile.  LDS: one staging buffer of the tile's keys (values reuse it
+// afterwards), per-wave digit counters -- 37 KB, so 4 workgroups fit a CU.
 // Global offsets: tile_prefix[d][tile] (per-digit exclusive scan over tiles) + exclusive scan
 // of the digit totals.  (A single-pass decoupled look-back variant measured slower on MI355X:
 // the chained tile-to-tile hand-off crosses the non-coherent per-XCD L2s at every hop.)
@@ -242,18 +246,18 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
                                                                const uint32_t* __restrict__ tile_prefix,
                                                                const uint32_t* __restrict__ totals)
 {
-    __shared__ __attribute__((aligned(16))) K s_keys[kTile];
-    __shared__ __attribute__((aligned(16))) uint32_t s_vals[kTile];
+    __shared__ __attribute__((aligned(16))) K s_stage[kTile];  // keys by tile-local rank, then values
     __shared__ uint32_t s_cnt[kWavesPerBlock][kRadix];  // per-wave running counters, later global offsets
     __shared__ uint32_t s_start[kRadix];                // tile-local start of each digit run
     __shared__ uint32_t s_wave[kWavesPerBlock];
+    uint32_t* s_vals = reinterpret_cast<uint32_t*>(s_stage);
 
     const int t = threadIdx.x;
     const int lane = lane_id();
     const int wave = t / kWave;
     for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
     const long long base = (long long)blockIdx.x * kTile;
-    const long long seg = base + (long long)wave * (kItems * kWave);  // this wave's 1024 items
+    const long long seg = base + (long long)wave * (kItems * kWave);  // this wave's items
 
     K k[kItems];
     uint32_t v[kItems];
@@ -275,13 +279,13 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
     uint32_t dummy;
     s_start[d] = block_exclusive_scan(tile_count_d, s_wave, &dummy);
     __syncthreads();
+    uint32_t pos[kItems];
 #pragma unroll
     for (int r = 0; r < kItems; r++) {
         if (ok[r]) {
             const uint32_t dd = digit_of(k[r], shift, mask);
-            const uint32_t pos = s_start[dd] + s_cnt[wave][dd] + rank[r];
-            s_keys[pos] = k[r];
-            s_vals[pos] = v[r];
+            pos[r] = s_start[dd] + s_cnt[wave][dd] + rank[r];
+            s_stage[pos[r]] = k[r];
         }
     }
     __syncthreads();
@@ -291,13 +295,26 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
     }
     __syncthreads();
     const int count = (int)((n - base) < kTile ? (n - base) : kTile);
-    for (int i = t; i < count; i += kBlock) {
-        const K key = s_keys[i];
-        const uint32_t dst = s_cnt[0][digit_of(key, shift, mask)] + i;
-        if (dst < n) {  // always true for consistent counts; never write outside the output
-            keys_out[dst] = key;
-            vals_out[dst] = s_vals[i];
+    uint32_t dst[kItems];
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {  // keys, run-contiguous: position i = t + 256 j
+        const int i = t + j * kBlock;
+        dst[j] = 0xffffffffu;
+        if (i < count) {
+            const K key = s_stage[i];
+            dst[j] = s_cnt[0][digit_of(key, shift, mask)] + i;
+            if (dst[j] < n) keys_out[dst[j]] = key;  // always true for consistent counts
         }
+    }
+    __syncthreads();  // every key read: the staging buffer takes the values
+#pragma unroll
+    for (int r = 0; r < kItems; r++)
+        if (ok[r]) s_vals[pos[r]] = v[r];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        const int i = t + j * kBlock;
+        if (i < count && dst[j] < n) vals_out[dst[j]] = s_vals[i];
     }
 }
 
@@ -614,22 +631,44 @@ __global__ __launch_bounds__(kBlock) void segment_sort_big_kernel(uint64_t* __re
 // than written out of bounds.
 // tile = (key >> 32) & tile_mask (the public entry point passes all ones; the segmented sort
 // masks to its segment bits).
+// ranges[tile] = [first, last + 1) of the tile's keys (tile = (key >> 32) & tile_mask); tiles
+// >= num_tiles are skipped.  Each thread checks 4 consecutive keys (two 16-byte loads) and the
+// key before them; only the rare boundaries write.
+constexpr int kRangeKeys = 4;
 __global__ __launch_bounds__(kBlock) void identify_ranges_kernel(const uint64_t* __restrict__ keys, long long n,
                                                                  uint2* __restrict__ ranges, uint32_t num_tiles,
                                                                  uint32_t tile_mask)
 {
-    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t cur = (uint32_t)(keys[i] >> 32) & tile_mask;
-    if (i == 0) {
-        if (cur < num_tiles) ranges[cur].x = 0;
+    const long long i0 = ((long long)blockIdx.x * kBlock + threadIdx.x) * kRangeKeys;
+    if (i0 >= n) return;
+    uint32_t tile[kRangeKeys];
+    if (i0 + kRangeKeys <= n && (reinterpret_cast<uintptr_t>(keys) & 15) == 0) {
+        const ulonglong2* k2 = reinterpret_cast<const ulonglong2*>(keys + i0);
+        const ulonglong2 a = k2[0], b = k2[1];
+        tile[0] = (uint32_t)(a.x >> 32) & tile_mask;
+        tile[1] = (uint32_t)(a.y >> 32) & tile_mask;
+        tile[2] = (uint32_t)(b.x >> 32) & tile_mask;
+        tile[3] = (uint32_t)(b.y >> 32) & tile_mask;
     } else {
-        const uint32_t prev = (uint32_t)(keys[i - 1] >> 32) & tile_mask;
-        if (cur != prev) {
-            if (prev < num_tiles) ranges[prev].y = (uint32_t)i;
-            if (cur < num_tiles) ranges[cur].x = (uint32_t)i;
+#pragma unroll
+        for (int j = 0; j < kRangeKeys; j++) tile[j] = i0 + j < n ? (uint32_t)(keys[i0 + j] >> 32) & tile_mask : 0u;
+    }
+    uint32_t prev = i0 == 0 ? 0u : (uint32_t)(keys[i0 - 1] >> 32) & tile_mask;
+#pragma unroll
+    for (int j = 0; j < kRangeKeys; j++) {
+        const long long i = i0 + j;
+        if (i >= n) break;
+        const uint32_t cur = tile[j];
+        if (i == 0) {  // the reference leaves .y of a single key's tile unset (n == 1)
+            if (cur < num_tiles) ranges[cur].x = 0;
+        } else {
+            if (cur != prev) {
+                if (prev < num_tiles) ranges[prev].y = (uint32_t)i;
+                if (cur < num_tiles) ranges[cur].x = (uint32_t)i;
+            }
+            if (i == n - 1 && cur < num_tiles) ranges[cur].y = (uint32_t)n;
         }
-        if (i == n - 1 && cur < num_tiles) ranges[cur].y = (uint32_t)n;
+        prev = cur;
     }
 }
 
@@ -728,7 +767,7 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         if (hipMemsetAsync(ranges, 0, sizeof(uint2) * nseg, stream) != hipSuccess ||
             hipMemsetAsync(n_overflow, 0, sizeof(uint32_t), stream) != hipSuccess)
             return fail(HIDEGS_E_HIP, std::string(what) + ": memset failed");
-        HIDEGS_LAUNCH("segment_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock)), dim3(kBlock), 0, stream,
+        HIDEGS_LAUNCH("segment_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock * kRangeKeys)), dim3(kBlock), 0, stream,
                       (const uint64_t*)ko, n, ranges, (uint32_t)nseg, (uint32_t)(nseg - 1));
         HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out, ranges,
                       overflow, n_overflow);
@@ -779,7 +818,7 @@ int identify_tile_ranges(const uint64_t* keys, long long n, uint32_t* ranges, in
         return fail(HIDEGS_E_HIP, "identify_tile_ranges: memset failed");
     if (n == 0) return check_launch("identify_tile_ranges", stream, 0);
     if (!keys) return fail(HIDEGS_E_ARG, "identify_tile_ranges: NULL keys");
-    HIDEGS_LAUNCH("identify_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock)), dim3(kBlock), 0, stream, keys, n,
+    HIDEGS_LAUNCH("identify_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock * kRangeKeys)), dim3(kBlock), 0, stream, keys, n,
                        reinterpret_cast<uint2*>(ranges), (uint32_t)num_tiles, 0xffffffffu);
     return check_launch("identify_tile_ranges", stream, 0);
 }

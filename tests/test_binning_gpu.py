@@ -125,12 +125,22 @@ def test_inclusive_scan_tiles_touched_like_and_in_place():
     assert np.array_equal(t.cpu().numpy().view(np.uint32), binning.inclusive_scan_u32(x))
 
 
-@pytest.mark.parametrize("K,T", [(0, 10), (1, 10), (2, 10), (8_000_000, 8160), (50_000, 32400)])
+@pytest.mark.parametrize("K,T", [(0, 10), (1, 10), (2, 10), (3, 10), (5, 3), (4097, 64), (8_000_000, 8160),
+                                 (8_000_003, 8160), (50_000, 32400)])
 def test_tile_ranges_bit_exact(K, T):
     keys, _ = raster_like_keys(K, T, 7)
     keys = np.sort(keys)
     got = primitives.identify_tile_ranges(u64(keys), T).cpu().numpy().view(np.uint32)
     assert np.array_equal(got, binning.tile_ranges(keys, T))
+
+
+def test_tile_ranges_of_an_unaligned_view():
+    """Keys starting 8 bytes into a buffer: the 16-byte vector loads give way to scalar ones."""
+    keys, _ = raster_like_keys(100_003, 640, 9)
+    keys = np.sort(keys)
+    buf = u64(np.concatenate([np.zeros(1, np.uint64), keys]))
+    got = primitives.identify_tile_ranges(buf[1:], 640).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, binning.tile_ranges(keys, 640))
 
 
 def test_binning_chain_scan_sort_ranges():
