@@ -315,7 +315,10 @@ __global__ __launch_bounds__(kBlock) void super_box_kernel(const Box* __restrict
 }
 
 // ---- 5. phase 1: one wave per leaf ------------------------------------------------------------
-constexpr int kGroups = 4;                  // query groups per wave for the coarse filter
+#ifndef HIDEGS_KNN_GROUPS
+#define HIDEGS_KNN_GROUPS 2
+#endif
+constexpr int kGroups = HIDEGS_KNN_GROUPS;  // query groups per wave for the coarse filter
 constexpr int kSuperBatch = 4;              // super-boxes tested per lane per batch
 constexpr int kLeafBatch = 4;               // passing super-boxes whose leaf boxes load together
 constexpr int kListCap = 256;               // candidate leaves buffered per wave
@@ -324,6 +327,9 @@ constexpr int kListCap = 256;               // candidate leaves buffered per wav
 #endif
 constexpr int kFlushBatch = HIDEGS_KNN_FLUSH_BATCH;  // candidate leaves loaded together
 constexpr int kGroupLanes = kWave / kGroups;
+#ifndef HIDEGS_KNN_SUBBOX_FILTER
+#define HIDEGS_KNN_SUBBOX_FILTER 1  // 0: no per-lane sub-box test before the point filter (A/B builds)
+#endif
 #ifndef HIDEGS_KNN_BAILOUT
 #define HIDEGS_KNN_BAILOUT 256
 #endif
@@ -475,9 +481,9 @@ __global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restri
                 for (int q = 0; q < kFlushBatch; q++) {
                     if (i0 + q >= cnt) break;
                     n_coarse++;
-                    uint32_t smask4 = 0;
+                    uint32_t smask4 = HIDEGS_KNN_SUBBOX_FILTER ? 0u : (1u << kSub) - 1u;
 #pragma unroll
-                    for (int j = 0; j < kSub; j++) {
+                    for (int j = 0; j < kSub && HIDEGS_KNN_SUBBOX_FILTER; j++) {
                         const Box sb{make_float4(uniform_lane(bx[q].x, 2 * j), uniform_lane(bx[q].y, 2 * j),
                                                  uniform_lane(bx[q].z, 2 * j), 0.f),
                                      make_float4(uniform_lane(bx[q].x, 2 * j + 1), uniform_lane(bx[q].y, 2 * j + 1),
