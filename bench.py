@@ -10,11 +10,12 @@ on (config 3: 2M Gaussians, one 1920x1080 view, synthetic D2 inputs resident in 
 
   step      = the binning stage of one view: inclusive scan of the 2M tiles_touched,
               stable radix sort of the K ~ 8M (tile|depth, id) pairs over bits
-              [0, 32 + getHigherMsb(8160)) = [0, 45), tile ranges (rasterizer_impl.cu:321-371).
+              [0, 32 + getHigherMsb(8160)) = [0, 45) and the tile ranges, as one
+              hidegs_sort_tile_pairs call (rasterizer_impl.cu:321-371).
               W warm-up steps, then K timed steps between HIP events on the launch stream,
               barrier + synchronize on both sides, max over ranks.
-  roofline  = the sort's scatter kernel (the dominant kernel of the step): 24 algorithmic
-              bytes per pair per launch (key 8 + value 4, read and written once), averaged
+  roofline  = the dominant kernel of the step (the most time per step): 24 algorithmic
+              bytes per pair per launch for a sort pass (key 8 + value 4, read and written once), averaged
               over its launches with per-launch HIP events (hidegs_kernel_timing), against
               8 TB/s; traffic from the committed rocprofv3 PMC summary when present.
   distCUDA2 = simple_knn._C.distCUDA2 on the 2M D2 centres (once-per-scene initialiser).
@@ -131,8 +132,7 @@ def main() -> None:
 
     def step():
         primitives.inclusive_scan_u32(wl.tiles_touched, out=offsets)
-        ko, vo = primitives.sort_pairs(wl.keys, wl.values, 0, end_bit)
-        primitives.identify_tile_ranges(ko, T)
+        primitives.sort_tile_pairs(wl.keys, wl.values, T)  # SortPairs + identifyTileRanges in one call
 
     ms_step, wall_ms_step = timed(step, args.steps, args.warmup)
 
@@ -163,7 +163,7 @@ def main() -> None:
     traffic = None
     rocprof_name = {"radix_scatter_u64": "radix_scatter_kernel", "segment_sort": "segment_sort_kernel",
                     "radix_hist_u64": "radix_hist_kernel"}.get(dom, dom + "_kernel")
-    grid = {"segment_sort": (1 << (end_bit - 32)) * 256}.get(dom, ((K + 4095) // 4096) * 256)
+    grid = {"segment_sort": T * 256}.get(dom, ((K + 4095) // 4096) * 256)
     if os.path.exists(TRAFFIC_FILE):
         with open(TRAFFIC_FILE) as f:
             traffic = json.load(f).get(f"{rocprof_name}@{grid}", {}).get("hbm_bytes_per_launch")

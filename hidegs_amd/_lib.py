@@ -62,6 +62,7 @@ SIGNATURES = {
     "hidegs_sort_pairs_u32_scratch_bytes": (SZ, [LL]),
     "hidegs_sort_pairs_u32": (I, [P, SZ, P, P, P, P, LL, I, I, P]),
     "hidegs_identify_tile_ranges": (I, [P, LL, P, I, P]),
+    "hidegs_sort_tile_pairs": (I, [P, SZ, P, P, P, P, LL, I, P, P]),
     "hidegs_higher_msb": (U32, [U32]),
     "hidegs_masked_adam": (I, [P, P, P, P, P, LL, I, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                                 LL, P]),

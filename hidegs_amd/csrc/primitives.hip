@@ -26,6 +26,8 @@
 #include "common.h"
 
 namespace hidegs {
+int identify_tile_ranges(const uint64_t* keys, long long n, uint32_t* ranges, int num_tiles, hipStream_t stream);
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -80,13 +82,25 @@ __global__ __launch_bounds__(kBlock) void scan_reduce_kernel(const uint32_t* __r
 }
 
 // in and out may alias (in-place scan): each workgroup reads its whole tile before writing it.
+// With `sums_raw` the workgroup adds up the tile sums before it itself (up to kOwnOffsetTiles
+// tiles: a few loads per thread), which saves the separate scan of the tile sums; otherwise
+// tile_offsets holds that exclusive scan.
+constexpr int kOwnOffsetTiles = 4096;
 __global__ __launch_bounds__(kBlock) void scan_downsweep_kernel(const uint32_t* in, long long n,
                                                                 const uint32_t* __restrict__ tile_offsets,
-                                                                uint32_t* out)
+                                                                int sums_raw, uint32_t* out)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_tile[kTile];
     __shared__ uint32_t s_wave[kWavesPerBlock];
     const long long base = (long long)blockIdx.x * kTile;
+    uint32_t tile_off;
+    if (sums_raw) {
+        uint32_t part = 0;
+        for (int i = threadIdx.x; i < (int)blockIdx.x; i += kBlock) part += tile_offsets[i];
+        block_exclusive_scan(part, s_wave, &tile_off);
+    } else {
+        tile_off = tile_offsets[blockIdx.x];
+    }
     load_tile_u32(in, base, n, s_tile);
     uint32_t v[kItems];
     uint32_t sum = 0;
@@ -96,7 +110,7 @@ __global__ __launch_bounds__(kBlock) void scan_downsweep_kernel(const uint32_t* 
         sum += v[j];
     }
     uint32_t total;
-    uint32_t run = block_exclusive_scan(sum, s_wave, &total) + tile_offsets[blockIdx.x];
+    uint32_t run = block_exclusive_scan(sum, s_wave, &total) + tile_off;
 #pragma unroll
     for (int j = 0; j < kItems; j++) {
         run += v[j];
@@ -429,58 +443,27 @@ __device__ __forceinline__ void wave_and_or(uint32_t& a, uint32_t& o)
     }
 }
 
-// Workgroup b sorts segment b (<= kSegCap pairs) in place by the low 32 key bits; larger
-// segments are appended to `overflow`.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void segment_sort_kernel(
-    uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint2* __restrict__ ranges,
-    uint32_t* __restrict__ overflow, uint32_t* __restrict__ n_overflow)
+// LSD form of the per-segment sort (the fallback of segment_sort_kernel for segments whose
+// depth bits crowd into a few buckets): run A (<= kSegRun) sorted in LDS, run B parked in registers
+// and sorted after it, the two merged by rank; every item's high key half and value gathered by
+// its index in the segment and written in place.  `diff` = the low key bits that vary.
+__device__ __forceinline__ void segment_sort_lsd(uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                 const uint32_t begin, const uint32_t m, const uint32_t diff,
+                                                 SegShared& sh)
 {
-    __shared__ __attribute__((aligned(16))) SegShared sh;
-    __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock];
-    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
-    const uint2 r = ranges[blockIdx.x];
-    const uint32_t begin = r.x, m = r.y - r.x;
-    if (r.y <= r.x + 1) return;  // absent or single pair: already in place
-    if (m > (uint32_t)kSegCap) {
-        if (t == 0) overflow[atomicAdd(n_overflow, 1u)] = blockIdx.x;
-        return;
-    }
+    const int t = threadIdx.x;
     const uint32_t na = m < (uint32_t)kSegRun ? m : (uint32_t)kSegRun, nb = m - na;
-    // low key halves: run A into LDS buffer 0, run B into registers; bits that vary
     uint32_t bk[kRunItems];
-    uint32_t a = 0xffffffffu, o = 0;
 #pragma unroll
     for (int q = 0; q < kRunItems; q++) {
         const uint32_t i = t + q * kBlock;
-        const uint32_t ka = i < na ? (uint32_t)keys[begin + i] : 0u;
-        bk[q] = i < nb ? (uint32_t)keys[begin + kSegRun + i] : 0u;
         if (i < na) {
-            sh.k[0][i] = ka;
+            sh.k[0][i] = (uint32_t)keys[begin + i];
             sh.i[0][i] = i;
-            a &= ka;
-            o |= ka;
         }
-        if (i < nb) {
-            a &= bk[q];
-            o |= bk[q];
-        }
-    }
-    wave_and_or(a, o);
-    if (lane == 0) {
-        s_and[wave] = a;
-        s_or[wave] = o;
+        bk[q] = i < nb ? (uint32_t)keys[begin + kSegRun + i] : 0u;
     }
     __syncthreads();
-    uint32_t diff;
-    {
-        uint32_t aa = 0xffffffffu, oo = 0;
-#pragma unroll
-        for (int w = 0; w < kWavesPerBlock; w++) {
-            aa &= s_and[w];
-            oo |= s_or[w];
-        }
-        diff = aa ^ oo;  // bits that vary over the segment
-    }
     const int ca = lds_radix_sort(sh, na, diff);
 
     // final (position, low key, index) of this thread's items: position t + 256 q
@@ -551,6 +534,169 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
         if (fok[q]) {
             keys[begin + fp[q]] = ((uint64_t)hi[q] << 32) | fk[q];
             vals[begin + fp[q]] = v[q];
+        }
+    }
+}
+
+// Bucket form (the common case).  The segment's top kBucketBits varying low-key bits pick a
+// bucket; a counting pass (LDS atomics, any order) gives every bucket its place, and each item's
+// place inside its bucket is its exact rank there by (key bits below the bucket digit, index in
+// segment) -- a 64-bit compare per bucket member.  Equal keys are therefore ordered by their input
+// index, which is the stable order; no ballots and three workgroup barriers in place of the LSD
+// form's four per 8-bit pass.  Each item's key and value stay in registers from the load to the
+// in-place store (every load of the segment precedes the first barrier).
+constexpr int kBucketBits = 10;
+constexpr int kBuckets = 1 << kBucketBits;
+constexpr int kMaxBucket = 128;  // a fuller bucket sends the segment to the LSD form
+constexpr int kIndexBits = 11;   // index in segment < kSegCap
+
+static_assert(kSegCap <= (1 << kIndexBits), "segment index must fit its field");
+
+struct BucketShared {
+    uint64_t comb[kSegCap];   // (key bits below the digit << kIndexBits) | index, grouped by bucket
+    uint32_t start[kBuckets];
+    uint32_t fill[kBuckets];  // histogram, then the running fill pointer (= bucket end after filling)
+};
+static_assert(2 * kBuckets >= kSegCap, "start + fill double as the value staging buffer");
+
+union SegLds {
+    SegShared lsd;
+    BucketShared bucket;
+};
+
+// Workgroup b sorts segment b (<= kSegCap pairs) in place by the low 32 key bits; larger
+// segments are appended to `overflow`.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void segment_sort_kernel(
+    uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint2* __restrict__ ranges,
+    uint32_t* __restrict__ overflow, uint32_t* __restrict__ n_overflow)
+{
+    __shared__ __attribute__((aligned(16))) SegLds lds;
+    __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock], s_max[kWavesPerBlock];
+    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
+    const uint2 r = ranges[blockIdx.x];
+    const uint32_t begin = r.x, m = r.y - r.x;
+    if (r.y <= r.x + 1) return;  // absent or single pair: already in place
+    if (m > (uint32_t)kSegCap) {
+        if (t == 0) overflow[atomicAdd(n_overflow, 1u)] = blockIdx.x;
+        return;
+    }
+    uint64_t k[kSegItems];
+    uint32_t v[kSegItems];
+    uint32_t a = 0xffffffffu, o = 0;
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            k[q] = keys[begin + i];
+            v[q] = vals[begin + i];
+            a &= (uint32_t)k[q];
+            o |= (uint32_t)k[q];
+        }
+    }
+    BucketShared& sh = lds.bucket;
+    for (int i = t; i < kBuckets; i += kBlock) sh.fill[i] = 0u;
+    wave_and_or(a, o);
+    if (lane == 0) {
+        s_and[wave] = a;
+        s_or[wave] = o;
+    }
+    __syncthreads();
+    uint32_t diff;
+    {
+        uint32_t aa = 0xffffffffu, oo = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; w++) {
+            aa &= s_and[w];
+            oo |= s_or[w];
+        }
+        diff = aa ^ oo;  // low key bits that vary over the segment
+    }
+    if (diff == 0) return;  // equal low keys: the input order is the stable order
+    const int top = 31 - __builtin_clz(diff);
+    const int dbits = top + 1 < kBucketBits ? top + 1 : kBucketBits;
+    const int shift = top + 1 - dbits;
+    const uint32_t dmask = (1u << dbits) - 1u;
+    const uint32_t lowmask = (uint32_t)((1ull << shift) - 1ull);
+
+    // 1. bucket histogram
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++)
+        if (t + q * kBlock < m) atomicAdd(&sh.fill[((uint32_t)k[q] >> shift) & dmask], 1u);
+    __syncthreads();
+    // 2. bucket starts (exclusive scan, 4 buckets per thread) and the fullest bucket
+    uint32_t c[kBuckets / kBlock], sum = 0, mx = 0;
+#pragma unroll
+    for (int j = 0; j < kBuckets / kBlock; j++) {
+        c[j] = sh.fill[t * (kBuckets / kBlock) + j];
+        sum += c[j];
+        mx = c[j] > mx ? c[j] : mx;
+    }
+    uint32_t dummy;
+    uint32_t pre = block_exclusive_scan(sum, s_max, &dummy);  // its barriers order the reads above
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint32_t y = __shfl_xor(mx, s, kWave);
+        mx = y > mx ? y : mx;
+    }
+    if (lane == 0) s_and[wave] = mx;
+#pragma unroll
+    for (int j = 0; j < kBuckets / kBlock; j++) {
+        sh.start[t * (kBuckets / kBlock) + j] = pre;
+        sh.fill[t * (kBuckets / kBlock) + j] = pre;
+        pre += c[j];
+    }
+    __syncthreads();
+    uint32_t fullest = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; w++) fullest = s_and[w] > fullest ? s_and[w] : fullest;
+    if (fullest > (uint32_t)kMaxBucket) {  // crowded depths: the LSD form (block-uniform branch)
+        __syncthreads();
+        segment_sort_lsd(keys, vals, begin, m, diff, lds.lsd);
+        return;
+    }
+    // 3. fill the buckets in any order
+    uint64_t me[kSegItems];
+    uint32_t bucket[kSegItems];
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            bucket[q] = ((uint32_t)k[q] >> shift) & dmask;
+            me[q] = ((uint64_t)((uint32_t)k[q] & lowmask) << kIndexBits) | i;
+            sh.comb[atomicAdd(&sh.fill[bucket[q]], 1u)] = me[q];
+        }
+    }
+    __syncthreads();
+    // 4. exact rank inside the bucket
+    uint32_t pos[kSegItems];
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        if (t + q * kBlock < m) {
+            const uint32_t s0 = sh.start[bucket[q]], e0 = sh.fill[bucket[q]];
+            uint32_t rank = 0;
+            for (uint32_t j = s0; j < e0; j++) rank += sh.comb[j] < me[q] ? 1u : 0u;
+            pos[q] = s0 + rank;
+        }
+    }
+    // 5. stage (key, value) by final position in LDS, then store the segment contiguously (stores
+    //    straight from registers scatter 8- and 4-byte writes over the segment: 78 -> 50 us at 8M pairs)
+    __syncthreads();
+    uint64_t* stage_k = sh.comb;
+    uint32_t* stage_v = sh.start;  // start and fill are adjacent: kSegCap u32
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        if (t + q * kBlock < m) {
+            stage_k[pos[q]] = k[q];
+            stage_v[pos[q]] = v[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            keys[begin + i] = stage_k[i];
+            vals[begin + i] = stage_v[i];
         }
     }
 }
@@ -698,15 +844,20 @@ size_t sort_scratch(long long n)
 __global__ void identify_ranges_kernel(const uint64_t* __restrict__ keys, long long n, uint2* __restrict__ ranges,
                                        uint32_t num_tiles, uint32_t tile_mask);
 
+// ranges_out (num_tiles entries) set: the tile ranges of the sorted keys are written too, with
+// identify_tile_ranges' semantics; the caller guarantees key >> 32 < num_tiles.
 template <typename K>
 int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
-               uint32_t* vals_out, long long n, int begin_bit, int end_bit, hipStream_t stream, const char* what)
+               uint32_t* vals_out, long long n, int begin_bit, int end_bit, hipStream_t stream, const char* what,
+               uint2* ranges_out = nullptr, int num_tiles = 0)
 {
     const int kbits = (int)(8 * sizeof(K));
     if (n < 0 || begin_bit < 0 || end_bit > kbits || begin_bit > end_bit)
         return fail(HIDEGS_E_ARG, std::string(what) + ": bad size or bit range");
     if (n > 0x7fffffffLL) return fail(HIDEGS_E_ARG, std::string(what) + ": more than 2^31-1 items");
-    if (n == 0) return 0;
+    if (n == 0)
+        return ranges_out ? identify_tile_ranges(nullptr, 0, reinterpret_cast<uint32_t*>(ranges_out), num_tiles, stream)
+                          : 0;
     if (!keys_in || !keys_out || !vals_in || !vals_out)
         return fail(HIDEGS_E_ARG, std::string(what) + ": NULL key/value pointer");
     if (keys_out == keys_in || vals_out == vals_in)
@@ -719,7 +870,9 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         if (hipMemcpyAsync(keys_out, keys_in, n * sizeof(K), hipMemcpyDeviceToDevice, stream) != hipSuccess ||
             hipMemcpyAsync(vals_out, vals_in, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
             return fail(HIDEGS_E_HIP, std::string(what) + ": copy failed");
-        return 0;
+        return ranges_out ? identify_tile_ranges(reinterpret_cast<const uint64_t*>(keys_out), n,
+                                                 reinterpret_cast<uint32_t*>(ranges_out), num_tiles, stream)
+                          : 0;
     }
     const int nt = ceil_div(n, kTile);
     Carver c(scratch);
@@ -759,8 +912,16 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         shift += bits;
     }
     if (segmented) {
-        const int nseg = 1 << (end_bit - 32);
+        // the segments' ranges; with ranges_out they are the caller's tile ranges (tile ids
+        // < num_tiles <= 2^(end_bit-32) leave no bits above end_bit, so segment == tile)
+        int nseg = 1 << (end_bit - 32);
         uint2* ranges = c.take<uint2>((size_t)1 << kMaxSegmentBits);
+        uint32_t tile_mask = (uint32_t)(nseg - 1);
+        if (ranges_out) {
+            ranges = ranges_out;
+            nseg = num_tiles;
+            tile_mask = 0xffffffffu;
+        }
         uint32_t* overflow = c.take<uint32_t>((size_t)1 << kMaxSegmentBits);
         uint32_t* n_overflow = c.take<uint32_t>(1);
         uint64_t* ko = reinterpret_cast<uint64_t*>(keys_out);
@@ -768,11 +929,15 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
             hipMemsetAsync(n_overflow, 0, sizeof(uint32_t), stream) != hipSuccess)
             return fail(HIDEGS_E_HIP, std::string(what) + ": memset failed");
         HIDEGS_LAUNCH("segment_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock * kRangeKeys)), dim3(kBlock), 0, stream,
-                      (const uint64_t*)ko, n, ranges, (uint32_t)nseg, (uint32_t)(nseg - 1));
+                      (const uint64_t*)ko, n, ranges, (uint32_t)nseg, tile_mask);
         HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out, ranges,
                       overflow, n_overflow);
         HIDEGS_LAUNCH("segment_sort_big", segment_sort_big_kernel, dim3(nseg < 512 ? nseg : 512), dim3(kBlock), 0,
                       stream, ko, vals_out, reinterpret_cast<uint64_t*>(alt_k), alt_v, ranges, overflow, n_overflow);
+    } else if (ranges_out) {
+        if (int rc = check_launch(what, stream, 0)) return rc;
+        return identify_tile_ranges(reinterpret_cast<const uint64_t*>(keys_out), n,
+                                    reinterpret_cast<uint32_t*>(ranges_out), num_tiles, stream);
     }
     return check_launch(what, stream, 0);
 }
@@ -790,8 +955,10 @@ int inclusive_scan_u32(void* scratch, size_t scratch_bytes, const uint32_t* in, 
     Carver c(scratch);
     uint32_t* sums = c.take<uint32_t>(nt);
     HIDEGS_LAUNCH("scan_reduce", scan_reduce_kernel, dim3(nt), dim3(kBlock), 0, stream, in, n, sums);
-    HIDEGS_LAUNCH("scan_small", scan_small_kernel, dim3(1), dim3(kBlock), 0, stream, sums, nt, (uint32_t*)nullptr);
-    HIDEGS_LAUNCH("scan_downsweep", scan_downsweep_kernel, dim3(nt), dim3(kBlock), 0, stream, in, n, sums, out);
+    const int own = nt <= kOwnOffsetTiles;
+    if (!own)
+        HIDEGS_LAUNCH("scan_small", scan_small_kernel, dim3(1), dim3(kBlock), 0, stream, sums, nt, (uint32_t*)nullptr);
+    HIDEGS_LAUNCH("scan_downsweep", scan_downsweep_kernel, dim3(nt), dim3(kBlock), 0, stream, in, n, sums, own, out);
     return check_launch("inclusive_scan_u32", stream, 0);
 }
 
@@ -808,6 +975,17 @@ int sort_pairs_u32(void* scratch, size_t bytes, const uint32_t* ki, uint32_t* ko
                    long long n, int b, int e, hipStream_t s)
 {
     return sort_pairs<uint32_t>(scratch, bytes, ki, ko, vi, vo, n, b, e, s, "sort_pairs_u32");
+}
+
+int sort_tile_pairs(void* scratch, size_t bytes, const uint64_t* ki, uint64_t* ko, const uint32_t* vi, uint32_t* vo,
+                    long long n, int num_tiles, uint32_t* ranges, hipStream_t s)
+{
+    if (num_tiles < 1) return fail(HIDEGS_E_ARG, "sort_tile_pairs: num_tiles must be >= 1");
+    if (!ranges) return fail(HIDEGS_E_ARG, "sort_tile_pairs: NULL ranges");
+    const int end = 32 + (int)(32u - (uint32_t)__builtin_clz((uint32_t)num_tiles | 1u));  // 32 + getHigherMsb
+    if (end > 64) return fail(HIDEGS_E_ARG, "sort_tile_pairs: too many tiles");
+    return sort_pairs<uint64_t>(scratch, bytes, ki, ko, vi, vo, n, 0, end, s, "sort_tile_pairs",
+                                reinterpret_cast<uint2*>(ranges), num_tiles);
 }
 
 int identify_tile_ranges(const uint64_t* keys, long long n, uint32_t* ranges, int num_tiles, hipStream_t stream)
@@ -851,6 +1029,14 @@ int hidegs_sort_pairs_u32(void* scratch, size_t scratch_bytes, const uint32_t* k
 {
     return hidegs::sort_pairs_u32(scratch, scratch_bytes, keys_in, keys_out, vals_in, vals_out, n, begin_bit, end_bit,
                                   hidegs::as_stream(stream));
+}
+
+int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                           const uint32_t* vals_in, uint32_t* vals_out, long long n, int num_tiles, uint32_t* ranges,
+                           void* stream)
+{
+    return hidegs::sort_tile_pairs(scratch, scratch_bytes, keys_in, keys_out, vals_in, vals_out, n, num_tiles, ranges,
+                                   hidegs::as_stream(stream));
 }
 
 int hidegs_identify_tile_ranges(const uint64_t* sorted_keys, long long n, uint32_t* ranges, int num_tiles,

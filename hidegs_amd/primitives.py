@@ -79,6 +79,32 @@ def sort_pairs(keys: torch.Tensor, values: torch.Tensor, begin_bit: int = 0,
     return ko, vo
 
 
+def sort_tile_pairs(keys: torch.Tensor, values: torch.Tensor,
+                    num_tiles: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """The reference's SortPairs + memset + identifyTileRanges (rasterizer_impl.cu:354-371) in one
+    call: pairs sorted over [0, 32 + getHigherMsb(num_tiles)) and the (num_tiles, 2) tile ranges.
+
+    keys are (tile << 32 | depth bits) with tile < num_tiles.  The same results as sort_pairs
+    followed by identify_tile_ranges; the per-tile ranges the sort computes anyway are the output.
+    """
+    if keys.dtype not in (torch.int64, torch.uint64) or keys.dim() != 1:
+        raise RuntimeError("sort_tile_pairs takes 1-D 64-bit keys")
+    if values.dtype not in (torch.int32, torch.uint32) or values.dim() != 1 or values.numel() != keys.numel():
+        raise RuntimeError("sort_tile_pairs takes 32-bit values, one per key")
+    n = keys.numel()
+    dev = _lib.device_of(keys, values) if n else _lib.device_of(keys)
+    ko, vo = torch.empty_like(keys), torch.empty_like(values)
+    ranges = torch.empty((int(num_tiles), 2), dtype=torch.int32, device=dev)
+    ki, vi = keys.contiguous(), values.contiguous()
+    L = _lib.lib()
+    with torch.cuda.device(dev):
+        tmp = _scratch(L.hidegs_sort_pairs_u64_scratch_bytes(n), dev)
+        rc = L.hidegs_sort_tile_pairs(_lib.ptr(tmp), tmp.numel(), _lib.ptr(ki), _lib.ptr(ko), _lib.ptr(vi),
+                                      _lib.ptr(vo), n, int(num_tiles), _lib.ptr(ranges), _lib.stream_handle(dev))
+        _lib.check(rc, "sort_tile_pairs")
+    return ko, vo, ranges
+
+
 def identify_tile_ranges(sorted_keys: torch.Tensor, num_tiles: int) -> torch.Tensor:
     """(num_tiles, 2) int32 [start, end) of each tile (key >> 32) in the sorted list."""
     if sorted_keys.dtype not in (torch.int64, torch.uint64) or sorted_keys.dim() != 1:

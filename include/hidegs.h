@@ -21,6 +21,7 @@
  *   hidegs_sort_pairs_u64/_u32  <- cub::DeviceRadixSort::SortPairs (HR/cuda_rasterizer/rasterizer_impl.cu:193-196,354-362;
  *                                  SK/simple_knn.cu:211-214)
  *   hidegs_identify_tile_ranges <- cudaMemsetAsync(ranges) + identifyTileRanges (HR/cuda_rasterizer/rasterizer_impl.cu:364-371,120-142)
+ *   hidegs_sort_tile_pairs      <- SortPairs + memset + identifyTileRanges as one call (rasterizer_impl.cu:354-371)
  *   hidegs_higher_msb           <- getHigherMsb (HR/cuda_rasterizer/rasterizer_impl.cu:35-50)
  *   hidegs_masked_adam          <- the per-parameter update of scene/OurAdam.py (_single_tensor_adam :249-337,
  *                                  _single_tensor_adam2 :340-420)
@@ -138,6 +139,18 @@ int hidegs_sort_pairs_u32(void* scratch, size_t scratch_bytes, const uint32_t* k
  */
 int hidegs_identify_tile_ranges(const uint64_t* sorted_keys, long long n, uint32_t* ranges, int num_tiles,
                                 void* stream);
+
+/*
+ * The binning sort as the reference's forward runs it -- SortPairs over [0, 32 + getHigherMsb(num_tiles)),
+ * the memset of the ranges and identifyTileRanges (HR/cuda_rasterizer/rasterizer_impl.cu:354-371) --
+ * in one call: the same keys_out, vals_out and ranges (num_tiles uint2) as hidegs_sort_pairs_u64
+ * followed by hidegs_identify_tile_ranges.  Keys are (tile << 32) | depth bits with tile < num_tiles.
+ * The sort partitions the pairs by tile anyway; the partition's ranges are the output, so the
+ * separate range pass is saved.  scratch: hidegs_sort_pairs_u64_scratch_bytes(n).
+ */
+int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                           const uint32_t* vals_in, uint32_t* vals_out, long long n, int num_tiles, uint32_t* ranges,
+                           void* stream);
 
 /* [host] getHigherMsb: bits needed to hold n, at least 1; the sort end bit is 32 + this of the tile count. */
 uint32_t hidegs_higher_msb(uint32_t n);

@@ -158,3 +158,48 @@ def test_binning_chain_scan_sort_ranges():
     tiles = (ko.cpu().numpy().view(np.uint64) >> np.uint64(32)).astype(np.int64)
     for t in np.flatnonzero(present)[:50]:
         assert (tiles[r[t, 0]:r[t, 1]] == t).all()
+
+
+@pytest.mark.parametrize("crowd", [100, 128, 129, 700, 2000])
+def test_segmented_sort_crowded_buckets_bit_exact(crowd):
+    """The per-tile sort buckets a segment by its top 10 varying depth bits and ranks inside each
+    bucket; a bucket of more than 128 pairs sends the segment to the LSD form.  `crowd` pairs of
+    each tile share their top depth bits (distinct low bits and exact duplicates), the rest spread
+    over the whole range, so both forms and the 128 / 129 boundary are exercised."""
+    T = 96
+    g = np.random.default_rng(crowd)
+    per_tile = crowd + 300
+    tiles = np.repeat(np.arange(T, dtype=np.uint64), per_tile)
+    base = np.float32(7.25).view(np.uint32)
+    depth = g.uniform(0.5, 80.0, tiles.size).astype(np.float32).view(np.uint32).astype(np.uint64)
+    crowded = (np.arange(tiles.size) % per_tile) < crowd
+    low = g.integers(0, 1 << 12, int(crowded.sum())).astype(np.uint64)
+    low[::5] = 17  # exact duplicates inside the crowded bucket
+    depth[crowded] = np.uint64(base & 0xFFFFF000) | low
+    order = g.permutation(tiles.size)
+    keys = ((tiles << np.uint64(32)) | depth)[order]
+    vals = np.arange(keys.size, dtype=np.uint32)
+    if keys.size < 65536:  # reach the segmented path
+        reps = 65536 // keys.size + 1
+        keys = np.concatenate([keys + (np.uint64(k * T) << np.uint64(32)) for k in range(reps)])
+        vals = np.arange(keys.size, dtype=np.uint32)
+    T_all = int(keys.max() >> np.uint64(32)) + 1
+    end = 32 + primitives.higher_msb(T_all)
+    ko, vo = primitives.sort_pairs(u64(keys), u32(vals), 0, end)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, end)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+
+
+@pytest.mark.parametrize("K,T", [(0, 10), (1, 10), (2, 64), (40_000, 64), (8_000_000, 8160), (2_000_000, 32400),
+                                 (300_000, 5)])
+def test_sort_tile_pairs_equals_sort_then_ranges(K, T):
+    """hidegs_sort_tile_pairs (sort + tile ranges in one call) against the oracle's stable sort over
+    [0, 32 + getHigherMsb(T)) and its range split."""
+    keys, vals = raster_like_keys(K, T, K + 3)
+    end = 32 + primitives.higher_msb(T)
+    ko, vo, r = primitives.sort_tile_pairs(u64(keys), u32(vals), T)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, end)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
