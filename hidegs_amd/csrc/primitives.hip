@@ -38,6 +38,7 @@ constexpr int kItems = HIDEGS_RADIX_ITEMS;
 constexpr int kTile = kBlock * kItems;       // 4096
 constexpr int kWavesPerBlock = kBlock / kWave;  // 4
 constexpr int kRadixBits = 8;
+
 constexpr int kRadix = 1 << kRadixBits;     // 256
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
@@ -199,15 +200,28 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const K* __restrict_
     __syncthreads();
     const long long base = (long long)blockIdx.x * kTile;
     K k[kItems];
+    if (sizeof(K) == 8 && base + kTile <= n && (reinterpret_cast<uintptr_t>(keys) & 15) == 0) {
+        // full tile: 16-byte loads, two keys each (the histogram does not care about item order)
+        const ulonglong2* k2 = reinterpret_cast<const ulonglong2*>(keys + base);
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
-        long long i = base + j * kBlock + t;
-        k[j] = (i < n) ? keys[i] : K(0);
-    }
+        for (int j = 0; j < kItems / 2; j++) {
+            const ulonglong2 p = k2[j * kBlock + t];
+            k[2 * j] = (K)p.x;
+            k[2 * j + 1] = (K)p.y;
+        }
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
-        long long i = base + j * kBlock + t;
-        if (i < n) atomicAdd(&s_hist[wave][digit_of(k[j], shift, mask)], 1u);
+        for (int j = 0; j < kItems; j++) atomicAdd(&s_hist[wave][digit_of(k[j], shift, mask)], 1u);
+    } else {
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            long long i = base + j * kBlock + t;
+            k[j] = (i < n) ? keys[i] : K(0);
+        }
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            long long i = base + j * kBlock + t;
+            if (i < n) atomicAdd(&s_hist[wave][digit_of(k[j], shift, mask)], 1u);
+        }
     }
     __syncthreads();
     for (int d = t; d < kRadix; d += kBlock) {
@@ -357,7 +371,7 @@ constexpr int kSegItems = kSegCap / kBlock;  // segment items per thread
 // LDS of one workgroup: two (low key, index-in-segment) buffers of one run plus ranking state.
 struct SegShared {
     uint32_t k[2][kSegRun];
-    uint32_t i[2][kSegRun];
+    uint16_t i[2][kSegRun];  // index in segment (< kSegCap)
     uint32_t cnt[kWavesPerBlock][kRadix];
     uint32_t start[kRadix];
     uint32_t wave[kWavesPerBlock];
@@ -440,6 +454,73 @@ __device__ __forceinline__ void wave_and_or(uint32_t& a, uint32_t& o)
     for (int sh = 32; sh >= 1; sh >>= 1) {
         a &= __shfl_xor(a, sh, kWave);
         o |= __shfl_xor(o, sh, kWave);
+    }
+}
+
+// LDS of the oversized-segment form.
+struct BigShared {
+    uint32_t cnt[kWavesPerBlock][kRadix];
+    uint32_t hist[kRadix];
+    uint32_t run[kRadix];  // running start of each digit within the segment
+    uint32_t wave[kWavesPerBlock];
+};
+
+// A segment of more than kSegCap pairs (a hot tile): 4 stable LSD passes over the low 32 bits
+// through global memory (keys/vals <-> alt within the segment's range), 2048 items per step (8 per
+// thread keeps the kernel inside the bucket form's register budget), by the segment's own workgroup.
+constexpr int kBigItems = 8;
+__device__ __forceinline__ void segment_sort_global(uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                    uint64_t* __restrict__ alt_k, uint32_t* __restrict__ alt_v,
+                                                    const uint32_t begin, const uint32_t m, BigShared& sh)
+{
+    const int t = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = t / kWave;
+    for (int pass = 0; pass < 4; pass++) {
+        const int shift = pass * kRadixBits;
+        const uint64_t* sk = (pass & 1) ? alt_k : keys;
+        const uint32_t* sv = (pass & 1) ? alt_v : vals;
+        uint64_t* dk = (pass & 1) ? keys : alt_k;
+        uint32_t* dv = (pass & 1) ? vals : alt_v;
+        sh.hist[t] = 0;
+        __syncthreads();
+        for (uint32_t i = t; i < m; i += kBlock) atomicAdd(&sh.hist[digit_of(sk[begin + i], shift, kRadix - 1)], 1u);
+        __syncthreads();
+        uint32_t dummy;
+        sh.run[t] = begin + block_exclusive_scan(sh.hist[t], sh.wave, &dummy);
+        __syncthreads();
+        for (uint32_t c0 = 0; c0 < m; c0 += (kBigItems * kBlock)) {
+            for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&sh.cnt[0][0])[i] = 0;
+            __syncthreads();
+            uint64_t k[kBigItems];
+            uint32_t v[kBigItems];
+            bool ok[kBigItems];
+            uint32_t rank[kBigItems];
+            const uint32_t w0 = c0 + wave * (kBigItems * kWave);
+#pragma unroll
+            for (int q = 0; q < kBigItems; q++) {
+                const uint32_t i = w0 + q * kWave + lane;
+                ok[q] = i < m;
+                k[q] = ok[q] ? sk[begin + i] : 0ull;
+                v[q] = ok[q] ? sv[begin + i] : 0u;
+            }
+            wave_rank<uint64_t, kBigItems>(k, ok, shift, kRadix - 1, sh.cnt[wave], rank, kRadix - 1);
+            __syncthreads();
+            const uint32_t tot = digit_wave_prefix(sh.cnt);
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < kBigItems; q++) {
+                if (ok[q]) {
+                    const uint32_t dd = digit_of(k[q], shift, kRadix - 1);
+                    const uint32_t dst = sh.run[dd] + sh.cnt[wave][dd] + rank[q];
+                    dk[dst] = k[q];
+                    dv[dst] = v[q];
+                }
+            }
+            __syncthreads();
+            sh.run[t] += tot;
+            __syncthreads();
+        }
     }
 }
 
@@ -541,7 +622,8 @@ __device__ __forceinline__ void segment_sort_lsd(uint64_t* __restrict__ keys, ui
 // Bucket form (the common case).  The segment's top kBucketBits varying low-key bits pick a
 // bucket; a counting pass (LDS atomics, any order) gives every bucket its place, and each item's
 // place inside its bucket is its exact rank there by (key bits below the bucket digit, index in
-// segment) -- a 64-bit compare per bucket member.  Equal keys are therefore ordered by their input
+// segment) -- one 32-bit compare per bucket member (the two fields fit 32 bits when the top
+// varying bit is <= 30, as for the float bits of positive depths; otherwise the LSD form runs).  Equal keys are therefore ordered by their input
 // index, which is the stable order; no ballots and three workgroup barriers in place of the LSD
 // form's four per 8-bit pass.  Each item's key and value stay in registers from the load to the
 // in-place store (every load of the segment precedes the first barrier).
@@ -549,26 +631,33 @@ constexpr int kBucketBits = 10;
 constexpr int kBuckets = 1 << kBucketBits;
 constexpr int kMaxBucket = 128;  // a fuller bucket sends the segment to the LSD form
 constexpr int kIndexBits = 11;   // index in segment < kSegCap
+#ifndef HIDEGS_SEG_WAVES
+#define HIDEGS_SEG_WAVES 7  // waves per SIMD the register budget is set for (17 KB of LDS allows 9)
+#endif
 
 static_assert(kSegCap <= (1 << kIndexBits), "segment index must fit its field");
 
 struct BucketShared {
-    uint64_t comb[kSegCap];   // (key bits below the digit << kIndexBits) | index, grouped by bucket
+    uint32_t comb[kSegCap];   // (key bits below the digit << kIndexBits) | index, grouped by bucket
     uint32_t start[kBuckets];
     uint32_t fill[kBuckets];  // histogram, then the running fill pointer (= bucket end after filling)
 };
-static_assert(2 * kBuckets >= kSegCap, "start + fill double as the value staging buffer");
+// after ranking, the whole struct stages the sorted segment: keys (u64) then values (u32) when
+// they fit together (<= kSegRun pairs), else keys and values one after the other
+static_assert(sizeof(BucketShared) >= kSegCap * sizeof(uint64_t), "staging of the keys");
+static_assert(sizeof(BucketShared) >= kSegRun * (sizeof(uint64_t) + sizeof(uint32_t)), "staging of a run");
 
 union SegLds {
     SegShared lsd;
     BucketShared bucket;
+    BigShared big;
 };
 
-// Workgroup b sorts segment b (<= kSegCap pairs) in place by the low 32 key bits; larger
-// segments are appended to `overflow`.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void segment_sort_kernel(
+// Workgroup b sorts segment b in place by the low 32 key bits: the bucket form, its LSD fallback
+// for crowded buckets, or (more than kSegCap pairs) the global form through alt_k / alt_v.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_SEG_WAVES))) void segment_sort_kernel(
     uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint2* __restrict__ ranges,
-    uint32_t* __restrict__ overflow, uint32_t* __restrict__ n_overflow)
+    uint64_t* __restrict__ alt_k, uint32_t* __restrict__ alt_v)
 {
     __shared__ __attribute__((aligned(16))) SegLds lds;
     __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock], s_max[kWavesPerBlock];
@@ -577,7 +666,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     const uint32_t begin = r.x, m = r.y - r.x;
     if (r.y <= r.x + 1) return;  // absent or single pair: already in place
     if (m > (uint32_t)kSegCap) {
-        if (t == 0) overflow[atomicAdd(n_overflow, 1u)] = blockIdx.x;
+        segment_sort_global(keys, vals, alt_k, alt_v, begin, m, lds.big);
         return;
     }
     uint64_t k[kSegItems];
@@ -649,20 +738,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     uint32_t fullest = 0;
 #pragma unroll
     for (int w = 0; w < kWavesPerBlock; w++) fullest = s_and[w] > fullest ? s_and[w] : fullest;
-    if (fullest > (uint32_t)kMaxBucket) {  // crowded depths: the LSD form (block-uniform branch)
+    if (fullest > (uint32_t)kMaxBucket || shift + kIndexBits > 32) {  // crowded depths, or fields too
+        // wide for 32 bits: the LSD form (block-uniform branch)
         __syncthreads();
         segment_sort_lsd(keys, vals, begin, m, diff, lds.lsd);
         return;
     }
     // 3. fill the buckets in any order
-    uint64_t me[kSegItems];
+    uint32_t me[kSegItems];
     uint32_t bucket[kSegItems];
 #pragma unroll
     for (int q = 0; q < kSegItems; q++) {
         const uint32_t i = t + q * kBlock;
         if (i < m) {
             bucket[q] = ((uint32_t)k[q] >> shift) & dmask;
-            me[q] = ((uint64_t)((uint32_t)k[q] & lowmask) << kIndexBits) | i;
+            me[q] = (((uint32_t)k[q] & lowmask) << kIndexBits) | i;
             sh.comb[atomicAdd(&sh.fill[bucket[q]], 1u)] = me[q];
         }
     }
@@ -681,13 +771,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     // 5. stage (key, value) by final position in LDS, then store the segment contiguously (stores
     //    straight from registers scatter 8- and 4-byte writes over the segment: 78 -> 50 us at 8M pairs)
     __syncthreads();
-    uint64_t* stage_k = sh.comb;
-    uint32_t* stage_v = sh.start;  // start and fill are adjacent: kSegCap u32
+    uint64_t* stage_k = reinterpret_cast<uint64_t*>(&sh);
+    uint32_t* stage_v = reinterpret_cast<uint32_t*>(stage_k + kSegRun);
+    const bool together = m <= (uint32_t)kSegRun;  // block-uniform
 #pragma unroll
     for (int q = 0; q < kSegItems; q++) {
         if (t + q * kBlock < m) {
             stage_k[pos[q]] = k[q];
-            stage_v[pos[q]] = v[q];
+            if (together) stage_v[pos[q]] = v[q];
         }
     }
     __syncthreads();
@@ -696,78 +787,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         const uint32_t i = t + q * kBlock;
         if (i < m) {
             keys[begin + i] = stage_k[i];
-            vals[begin + i] = stage_v[i];
+            if (together) vals[begin + i] = stage_v[i];
         }
     }
-}
-
-// One workgroup per oversized segment: 4 stable LSD passes over the low 32 bits through
-// global memory (keys/vals <-> alt within the segment's range), 4096 items per step.
-__global__ __launch_bounds__(kBlock) void segment_sort_big_kernel(uint64_t* __restrict__ keys,
-                                                                  uint32_t* __restrict__ vals,
-                                                                  uint64_t* __restrict__ alt_k,
-                                                                  uint32_t* __restrict__ alt_v,
-                                                                  const uint2* __restrict__ ranges,
-                                                                  const uint32_t* __restrict__ overflow,
-                                                                  const uint32_t* __restrict__ n_overflow)
-{
-    __shared__ uint32_t s_cnt[kWavesPerBlock][kRadix];
-    __shared__ uint32_t s_hist[kRadix];
-    __shared__ uint32_t s_run[kRadix];  // running global start of each digit within the segment
-    __shared__ uint32_t s_wave[kWavesPerBlock];
-    const int t = threadIdx.x;
-    const int lane = lane_id();
-    const int wave = t / kWave;
-    const uint32_t nover = *n_overflow;
-    for (uint32_t o = blockIdx.x; o < nover; o += gridDim.x) {
-        const uint2 r = ranges[overflow[o]];
-        const uint32_t begin = r.x, m = r.y - r.x;
-        for (int pass = 0; pass < 4; pass++) {
-            const int shift = pass * kRadixBits;
-            const uint64_t* sk = (pass & 1) ? alt_k : keys;
-            const uint32_t* sv = (pass & 1) ? alt_v : vals;
-            uint64_t* dk = (pass & 1) ? keys : alt_k;
-            uint32_t* dv = (pass & 1) ? vals : alt_v;
-            s_hist[t] = 0;
-            __syncthreads();
-            for (uint32_t i = t; i < m; i += kBlock) atomicAdd(&s_hist[digit_of(sk[begin + i], shift, kRadix - 1)], 1u);
-            __syncthreads();
-            uint32_t dummy;
-            s_run[t] = begin + block_exclusive_scan(s_hist[t], s_wave, &dummy);
-            __syncthreads();
-            for (uint32_t c0 = 0; c0 < m; c0 += kTile) {
-                for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
-                __syncthreads();
-                uint64_t k[kItems];
-                uint32_t v[kItems];
-                bool ok[kItems];
-                uint32_t rank[kItems];
-                const uint32_t w0 = c0 + wave * (kItems * kWave);
+    if (together) return;
+    __syncthreads();
+    stage_v = reinterpret_cast<uint32_t*>(&sh);
 #pragma unroll
-                for (int q = 0; q < kItems; q++) {
-                    const uint32_t i = w0 + q * kWave + lane;
-                    ok[q] = i < m;
-                    k[q] = ok[q] ? sk[begin + i] : 0ull;
-                    v[q] = ok[q] ? sv[begin + i] : 0u;
-                }
-                wave_rank<uint64_t, kItems>(k, ok, shift, kRadix - 1, s_cnt[wave], rank, kRadix - 1);
-                __syncthreads();
-                const uint32_t tot = digit_wave_prefix(s_cnt);
-                __syncthreads();
+    for (int q = 0; q < kSegItems; q++)
+        if (t + q * kBlock < m) stage_v[pos[q]] = v[q];
+    __syncthreads();
 #pragma unroll
-                for (int q = 0; q < kItems; q++) {
-                    if (ok[q]) {
-                        const uint32_t dd = digit_of(k[q], shift, kRadix - 1);
-                        const uint32_t dst = s_run[dd] + s_cnt[wave][dd] + rank[q];
-                        dk[dst] = k[q];
-                        dv[dst] = v[q];
-                    }
-                }
-                __syncthreads();
-                s_run[t] += tot;
-                __syncthreads();
-            }
-        }
+    for (int q = 0; q < kSegItems; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) vals[begin + i] = stage_v[i];
     }
 }
 
@@ -835,9 +868,8 @@ size_t sort_scratch(long long n)
     const int nt = ceil_div(n, kTile);
     size_t b = align_up((size_t)n * sizeof(K)) + align_up((size_t)n * sizeof(uint32_t)) +
                align_up((size_t)kRadix * nt * sizeof(uint32_t)) + align_up(kRadix * sizeof(uint32_t));
-    if (sizeof(K) == 8)  // segmented path: ranges, overflow list and its counter
-        b += align_up(sizeof(uint2) << kMaxSegmentBits) + align_up(sizeof(uint32_t) << kMaxSegmentBits) +
-             align_up(sizeof(uint32_t));
+    if (sizeof(K) == 8)  // segmented path: the segment ranges
+        b += align_up(sizeof(uint2) << kMaxSegmentBits);
     return b;
 }
 
@@ -922,18 +954,13 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
             nseg = num_tiles;
             tile_mask = 0xffffffffu;
         }
-        uint32_t* overflow = c.take<uint32_t>((size_t)1 << kMaxSegmentBits);
-        uint32_t* n_overflow = c.take<uint32_t>(1);
         uint64_t* ko = reinterpret_cast<uint64_t*>(keys_out);
-        if (hipMemsetAsync(ranges, 0, sizeof(uint2) * nseg, stream) != hipSuccess ||
-            hipMemsetAsync(n_overflow, 0, sizeof(uint32_t), stream) != hipSuccess)
+        if (hipMemsetAsync(ranges, 0, sizeof(uint2) * nseg, stream) != hipSuccess)
             return fail(HIDEGS_E_HIP, std::string(what) + ": memset failed");
         HIDEGS_LAUNCH("segment_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock * kRangeKeys)), dim3(kBlock), 0, stream,
                       (const uint64_t*)ko, n, ranges, (uint32_t)nseg, tile_mask);
         HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out, ranges,
-                      overflow, n_overflow);
-        HIDEGS_LAUNCH("segment_sort_big", segment_sort_big_kernel, dim3(nseg < 512 ? nseg : 512), dim3(kBlock), 0,
-                      stream, ko, vals_out, reinterpret_cast<uint64_t*>(alt_k), alt_v, ranges, overflow, n_overflow);
+                      reinterpret_cast<uint64_t*>(alt_k), alt_v);
     } else if (ranges_out) {
         if (int rc = check_launch(what, stream, 0)) return rc;
         return identify_tile_ranges(reinterpret_cast<const uint64_t*>(keys_out), n,

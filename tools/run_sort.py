@@ -11,6 +11,6 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 wl = synthetic.binning_workload(2_000_000, device="cuda")
 end = 32 + primitives.higher_msb(wl.num_tiles)
 for _ in range(reps):
-    primitives.sort_pairs(wl.keys, wl.values, 0, end)
+    primitives.sort_tile_pairs(wl.keys, wl.values, wl.num_tiles)
 torch.cuda.synchronize()
 print("ok", wl.num_pairs)

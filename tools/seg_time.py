@@ -17,7 +17,7 @@ with _lib.kernel_timer() as kt:
         primitives.sort_pairs(wl.keys, wl.values, 0, end)
     torch.cuda.synchronize()
     out = []
-    for nm in ("radix_scatter_u64", "segment_sort", "segment_sort_2k", "segment_sort_big", "segment_classify"):
+    for nm in ("radix_hist_u64", "radix_digit_scan", "radix_scatter_u64", "segment_ranges", "segment_sort", "scan_reduce", "scan_downsweep"):
         ms, n = kt.get(nm)
         if n:
             out.append(f"{nm} {ms * 1e3 / n:.1f}us")
