@@ -21,6 +21,8 @@ on (config 3: 2M Gaussians, one 1920x1080 view, synthetic D2 inputs resident in 
   distCUDA2 = simple_knn._C.distCUDA2 on the 2M D2 centres (once-per-scene initialiser).
   exchange  = the view-DP exchange of 2M x 59 fp32 leaf gradients + stats over RCCL
               (a one-rank group at N = 1), HIP-event timed.
+  exchange_and_step = the exchange followed by the masked step, in sequence and overlapped bucket
+              by bucket (ViewDPExchange.exchange_and_step); at N = 1 neither exchanges anything.
   masked Adam = the fused row-masked optimizer step (hidegs_amd.optim.Adam, the OurAdam
               drop-in) over the six HiDeGS parameter groups at 2M Gaussians (59 fp32 each), 90%
               of rows visible; 28 algorithmic bytes per updated value; beside it the reference's
@@ -267,6 +269,25 @@ def main() -> None:
                                "hbm_frac": round(ad_bytes / (ad_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                                "reference_torch_ops_ms": round(ref_ms, 3),
                                "speedup_vs_reference_ops": round(ref_ms / ad_ms, 2)}
+        # the exchange and the step after it, in sequence and overlapped bucket by bucket
+        if not args.no_exchange:
+            arena = GradArena(N_GAUSSIANS, device=dev)
+            for k, p in prm.items():
+                arena[k].copy_(p.grad)
+            arena.attach(prm)
+            ex = ViewDPExchange()
+            norm = torch.rand(N_GAUSSIANS, 1, device=dev, generator=g)
+
+            def seq_step():
+                res = ex.exchange(arena, vis, max_stats=[norm])
+                opt.step(res.union)
+
+            seq_ms, _ = timed(seq_step, 10, 2)
+            fused_ms, _ = timed(lambda: ex.exchange_and_step(arena, vis, opt, prm, max_stats=[norm]), 10, 2)
+            line["exchange_and_step"] = {"world": world, "sequential_ms": round(seq_ms, 3),
+                                         "overlapped_ms": round(fused_ms, 3),
+                                         "collectives": ex.last.collectives, "union_rows": ex.last.union_rows}
+            del arena
         del prm, opt, st
 
     # ---- CPU baseline (rank 0, N = 1): the oracle's stable sort on the same pairs -------------

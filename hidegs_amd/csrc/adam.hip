@@ -32,7 +32,10 @@ namespace hidegs {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kQuadsPerThread = 2;                      // two 16-byte vectors per tensor in flight
+#ifndef HIDEGS_ADAM_QUADS
+#define HIDEGS_ADAM_QUADS 2
+#endif
+constexpr int kQuadsPerThread = HIDEGS_ADAM_QUADS;      // 16-byte vectors per tensor in flight
 constexpr int kQuadsPerBlock = kBlock * kQuadsPerThread;  // 2048 elements per workgroup
 constexpr int kMaxTensors = 8;                          // tensors per launch
 

@@ -286,6 +286,9 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
     for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
     const long long base = (long long)blockIdx.x * kTile;
     const long long seg = base + (long long)wave * (kItems * kWave);  // this wave's items
+    // this tile's global digit offsets, loaded now so their latency hides behind the ranking (digits
+    // above `mask` read stale counts that no item uses)
+    const uint32_t digit_total = totals[t], digit_prefix = tile_prefix[(long long)t * ntiles + blockIdx.x];
 
     K k[kItems];
     uint32_t v[kItems];
@@ -318,8 +321,8 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
     }
     __syncthreads();
     {
-        const uint32_t dbase = block_exclusive_scan(totals[d], s_wave, &dummy);
-        s_cnt[0][d] = dbase + tile_prefix[(long long)d * ntiles + blockIdx.x] - s_start[d];
+        const uint32_t dbase = block_exclusive_scan(digit_total, s_wave, &dummy);
+        s_cnt[0][d] = dbase + digit_prefix - s_start[d];
     }
     __syncthreads();
     const int count = (int)((n - base) < kTile ? (n - base) : kTile);

@@ -12,6 +12,11 @@ csrc/adam.hip) that reads and writes every relevant element once, instead of the
 per-parameter boolean-index gathers, eight elementwise ops and scatters.  Results equal the reference's torch ops on the
 GPU bit for bit (tests/test_adam_gpu.py).  No CPU fallback: parameters must live on the GPU.
 
+`begin_step(relevant)` splits the step in two: it advances the counters and describes every
+parameter's update (an `AdamStepPlan`) without running it; the plan then runs whole or row range
+by row range.  The view-DP exchange uses the row ranges to update each gradient bucket as soon as
+its all-reduce has landed (hidegs_amd.view_dp.ViewDPExchange.exchange_and_step).
+
 Not supported, as in the reference's masked path, which fails on them with a shape error:
 amsgrad, maximize; capturable (a different op sequence) is not reproduced.
 """
@@ -21,6 +26,56 @@ import torch
 from torch.optim.optimizer import Optimizer
 
 from hidegs_amd import _lib
+
+
+class AdamStepPlan:
+    """One prepared optimizer step: every parameter's step counter has advanced and its update is
+    described (device pointers, mask, hyper-parameters), nothing has run yet.
+
+    run()                  the whole step, one launch per device (what Adam.step does)
+    run_rows(p, r0, r1)    the update of rows [r0, r1) of parameter p only
+    Each row of each parameter is updated by exactly one of these per plan; how the rows are split
+    does not change a bit of the result (the update is row-local).
+    """
+
+    def __init__(self):
+        self._entries = []  # (param, device, descriptor, tensors the descriptor points into)
+        self._index = {}
+
+    def _add(self, p, dev, desc, keep) -> None:
+        self._index[id(p)] = len(self._entries)
+        self._entries.append((p, dev, desc, keep))
+
+    def __len__(self) -> int:
+        return len(self._entries)
+
+    def run(self) -> None:
+        batches = {}
+        for _, dev, desc, _ in self._entries:
+            batches.setdefault(dev, []).append(desc)
+        L = _lib.lib()
+        for dev, descs in batches.items():
+            arr = (_lib.AdamTensor * len(descs))(*descs)
+            with torch.cuda.device(dev):
+                _lib.check(L.hidegs_masked_adam_multi(arr, len(descs), _lib.stream_handle(dev)), "masked Adam")
+
+    def run_rows(self, param, row_start: int, row_end: int) -> None:
+        i = self._index.get(id(param))
+        if i is None:
+            raise KeyError("parameter is not part of this step (no gradient, or another optimizer's)")
+        _, dev, d, _ = self._entries[i]
+        r0, r1 = int(row_start), int(row_end)
+        if not 0 <= r0 <= r1 <= d.rows:
+            raise ValueError(f"rows [{r0}, {r1}) outside the parameter's {d.rows} rows")
+        if r0 == r1:
+            return
+        off = 4 * r0 * d.width  # fp32 bytes
+        sub = _lib.AdamTensor(d.param + off, d.grad + off, d.exp_avg + off, d.exp_avg_sq + off,
+                              (d.relevant + r0) if d.relevant else None, r1 - r0, d.width, d.lr, d.beta1, d.beta2,
+                              d.eps, d.weight_decay, d.step)
+        arr = (_lib.AdamTensor * 1)(sub)
+        with torch.cuda.device(dev):
+            _lib.check(_lib.lib().hidegs_masked_adam_multi(arr, 1, _lib.stream_handle(dev)), "masked Adam")
 
 
 class Adam(Optimizer):
@@ -53,15 +108,11 @@ class Adam(Optimizer):
         return mask
 
     @torch.no_grad()
-    def step(self, relevant, closure=None):
-        loss = None
-        if closure is not None:
-            with torch.enable_grad():
-                loss = closure()
+    def begin_step(self, relevant) -> AdamStepPlan:
+        """Advance every parameter's step counter and describe its update; see AdamStepPlan."""
         dense = relevant.size(0) == 0
         masks = {}
-        batches = {}  # device -> tensor descriptors, one native call per device
-        keep = []     # tensors referenced by the descriptors stay alive until the call returns
+        plan = AdamStepPlan()
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
             for p in group["params"]:
@@ -88,15 +139,18 @@ class Adam(Optimizer):
                 for t in (p, p.grad, state["exp_avg"], state["exp_avg_sq"]):
                     if not t.is_contiguous() or t.dtype != torch.float32:
                         raise RuntimeError("masked Adam needs contiguous float32 parameters, grads and moments")
-                keep.append((p, p.grad, state["exp_avg"], state["exp_avg_sq"], mask))
-                batches.setdefault(dev, []).append(_lib.AdamTensor(
+                desc = _lib.AdamTensor(
                     _lib.ptr(p), _lib.ptr(p.grad), _lib.ptr(state["exp_avg"]), _lib.ptr(state["exp_avg_sq"]),
                     _lib.ptr(mask), rows, width, float(group["lr"]), float(beta1), float(beta2),
-                    float(group["eps"]), float(group["weight_decay"]), step))
-        L = _lib.lib()
-        for dev, descs in batches.items():
-            arr = (_lib.AdamTensor * len(descs))(*descs)
-            with torch.cuda.device(dev):
-                _lib.check(L.hidegs_masked_adam_multi(arr, len(descs), _lib.stream_handle(dev)), "masked Adam")
-        del keep
+                    float(group["eps"]), float(group["weight_decay"]), step)
+                plan._add(p, dev, desc, (p, p.grad, state["exp_avg"], state["exp_avg_sq"], mask))
+        return plan
+
+    @torch.no_grad()
+    def step(self, relevant, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self.begin_step(relevant).run()
         return loss

@@ -28,7 +28,13 @@ over xGMI is bound per link (~153 GB/s) and pays a fixed cost per collective.
 
 Backend: whatever process group is current -- "nccl" (RCCL on ROCm) on the GPU, "gloo" in
 the CPU tests.  Bitwise OR is formed from an all-gather of packed masks (RCCL has no
-bitwise reduction), which also yields the per-Gaussian view count.
+bitwise reduction), which also yields the per-Gaussian view count.  A one-rank group has
+nothing to exchange and issues no collective.
+
+`exchange_and_step` fuses the exchange with the masked optimizer step that follows it: each
+dense bucket's rows are updated as soon as that bucket's all-reduce lands, while the later
+buckets are still reducing (SURVEY §8(e) E2's overlap; the backward that would also overlap it is
+not built here).
 """
 from __future__ import annotations
 
@@ -132,6 +138,8 @@ class ViewDPExchange:
         if visible.dtype != torch.bool or visible.dim() != 1:
             raise ValueError("visible must be a 1-D bool mask")
         world = dist.get_world_size(self.group)
+        if world == 1:  # one view: nothing to exchange
+            return visible.clone(), visible.to(torch.float32).unsqueeze(1)
         bits = pack_mask(visible)
         flat = bits.new_empty((world * bits.numel(),))
         dist.all_gather_into_tensor(flat, bits, group=self.group)
@@ -142,6 +150,8 @@ class ViewDPExchange:
 
     # ---- leaf gradients -----------------------------------------------------------
     def _all_reduce_buckets(self, flat: torch.Tensor) -> None:
+        if dist.get_world_size(self.group) == 1:  # the sum over one rank is the tensor itself
+            return
         per = max(1, self.bucket_bytes // flat.element_size())
         works = [dist.all_reduce(flat[s:s + per], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
                  for s in range(0, flat.numel(), per)]
@@ -190,6 +200,8 @@ class ViewDPExchange:
                                            "the compacted exchange would desynchronise the replicas")
         else:
             self.last.union_rows = n
+        if dist.get_world_size(self.group) == 1:  # one rank: the sum is the input, in place already
+            return
         if rows is None:
             self.last.compacted = False
             if arena is not None:
@@ -221,7 +233,7 @@ class ViewDPExchange:
     def max_stats(self, stats: List[torch.Tensor]) -> None:
         """In-place MAX over ranks of per-step maxima, all in ONE collective."""
         stats = [s for s in stats if s is not None]
-        if not stats:
+        if not stats or dist.get_world_size(self.group) == 1:
             return
         flat = torch.cat([s.reshape(-1).to(torch.float32) for s in stats])
         dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=self.group)
@@ -249,5 +261,53 @@ class ViewDPExchange:
         union, count = self.gather_visibility(visible)
         g = grads if isinstance(grads, GradArena) else grads.values()
         self.sum_gradients(g, union)
+        self.max_stats(max_stats or [])
+        return ExchangeResult(union, count)
+
+    def exchange_and_step(self, arena: GradArena, visible: torch.Tensor, optimizer, params: Dict[str, torch.Tensor],
+                          max_stats: Optional[List[torch.Tensor]] = None) -> ExchangeResult:
+        """`exchange` followed by the masked optimizer step on the union, with the two overlapped.
+
+        optimizer  has `begin_step(relevant) -> plan` with `plan.run()` and `plan.run_rows(p, r0, r1)`
+                   (hidegs_amd.optim.Adam); it is stepped with relevant = the union mask.
+        params     {field name: parameter} whose `.grad` are the arena's views (GradArena.attach).
+
+        Dense exchange: every bucket is a row range of one field; all buckets' all-reduces are issued
+        first, then, bucket by bucket, the compute stream waits for that bucket's reduction and
+        updates its rows -- so the update of bucket b runs while buckets b+1... are still on the
+        wire, and only the last bucket's update is exposed.  The field order ends with the narrow
+        fields, so that last bucket is small.  The compacted exchange (few union rows) and a
+        one-rank group step once after the exchange.  The result is bit-identical to `exchange`
+        then `optimizer.step(union)`: the update is row-local and every row is updated once.
+        """
+        if not isinstance(arena, GradArena):
+            raise TypeError("exchange_and_step works on a GradArena")
+        missing = [k for k in arena.widths if k not in params]
+        if missing:
+            raise KeyError(f"no parameter for arena fields {missing}")
+        self.last = ExchangeStats()
+        union, count = self.gather_visibility(visible)
+        plan = optimizer.begin_step(union)
+        n = arena.n
+        world = dist.get_world_size(self.group)
+        nu = int(union.sum()) if n else 0
+        if world == 1 or n == 0 or nu < self.compact_below * n:
+            self.sum_gradients(arena, union)
+            plan.run()
+        else:
+            self.last.union_rows = nu
+            works = []
+            for name, w in arena.widths.items():
+                rows = max(4, (self.bucket_bytes // (4 * w)) // 4 * 4)  # 4-row multiples keep 16-byte alignment
+                view = arena.views[name]
+                for r0 in range(0, n, rows):
+                    r1 = min(n, r0 + rows)
+                    works.append((dist.all_reduce(view[r0:r1], op=dist.ReduceOp.SUM, group=self.group,
+                                                  async_op=True), name, r0, r1))
+            self.last.collectives += len(works)
+            self.last.reduced_bytes += arena.flat.numel() * arena.flat.element_size()
+            for work, name, r0, r1 in works:
+                work.wait()  # the current stream waits for this bucket; later buckets keep reducing
+                plan.run_rows(params[name], r0, r1)
         self.max_stats(max_stats or [])
         return ExchangeResult(union, count)

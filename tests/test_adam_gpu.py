@@ -175,3 +175,34 @@ def test_multi_tensor_rejects_bad_descriptor():
     arr = (_lib.AdamTensor * 1)(bad)
     with pytest.raises(RuntimeError, match="step counts from 1"):
         _lib.check(_lib.lib().hidegs_masked_adam_multi(arr, 1, _lib.stream_handle(dev)), "multi")
+
+
+def test_step_plan_row_ranges_equal_the_whole_step():
+    """AdamStepPlan.run_rows over any split of the rows (4-row multiples and ragged cuts, which drop
+    to the scalar path) gives bit-identical parameters and moments to one whole step."""
+    n = 10_003
+    init = make(n, 11)
+    g = torch.Generator().manual_seed(12)
+    a = {k: torch.nn.Parameter(v.clone().cuda()) for k, v in init.items()}
+    b = {k: torch.nn.Parameter(v.clone().cuda()) for k, v in init.items()}
+    opt_a = Adam([{"params": [a[k]], "lr": LRS[k]} for k in SHAPES], lr=0.0, eps=1e-15)
+    opt_b = Adam([{"params": [b[k]], "lr": LRS[k]} for k in SHAPES], lr=0.0, eps=1e-15)
+    cuts = [0, 4, 1000, 1001, 1004, 5003, 9996, n]
+    for step in range(3):
+        rel = (torch.rand(n, generator=g) < 0.6).cuda() if step != 1 else torch.zeros(0, dtype=torch.bool)
+        for k, s in SHAPES.items():
+            gr = torch.randn((n, *s), generator=g).cuda()
+            a[k].grad, b[k].grad = gr, gr.clone()
+        opt_a.step(rel)
+        plan = opt_b.begin_step(rel)
+        assert len(plan) == len(SHAPES)
+        for k in SHAPES:
+            for r0, r1 in zip(cuts, cuts[1:]):
+                plan.run_rows(b[k], r0, r1)
+    torch.cuda.synchronize()
+    for k in SHAPES:
+        assert torch.equal(a[k].detach(), b[k].detach()), k
+        for m in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(opt_a.state[a[k]][m], opt_b.state[b[k]][m]), (k, m)
+    with pytest.raises(ValueError):
+        opt_b.begin_step(torch.zeros(0, dtype=torch.bool)).run_rows(b["xyz"], 5, n + 1)

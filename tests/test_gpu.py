@@ -58,3 +58,40 @@ def test_view_dp_exchange_over_rccl_single_rank():
             assert torch.equal(grads[k], ref[k])
     finally:
         dist.destroy_process_group()
+
+
+def test_exchange_and_step_over_rccl_single_rank_equals_step():
+    """exchange_and_step on a one-rank RCCL group: no collective, and the masked step on the union
+    equals optimizer.step(visible) bit for bit."""
+    import torch.distributed as dist
+    from hidegs_amd.optim import Adam
+    from hidegs_amd.view_dp import LEAF_WIDTHS, GradArena, ViewDPExchange
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        n = 50_001
+        g = torch.Generator(device="cuda").manual_seed(3)
+        visible = torch.rand(n, device="cuda", generator=g) < 0.8
+        init = {k: torch.randn(n, w, device="cuda", generator=g) for k, w in LEAF_WIDTHS.items()}
+        grads = {k: torch.randn(n, w, device="cuda", generator=g) for k, w in LEAF_WIDTHS.items()}
+        pa = {k: torch.nn.Parameter(v.clone()) for k, v in init.items()}
+        pb = {k: torch.nn.Parameter(v.clone()) for k, v in init.items()}
+        arena = GradArena(n, device="cuda")
+        arena.attach(pb)
+        for k in LEAF_WIDTHS:
+            pa[k].grad = grads[k].clone()
+            arena[k].copy_(grads[k])
+        Adam(list(pa.values()), lr=0.01, eps=1e-15).step(visible)
+        ex = ViewDPExchange(compact_below=0.0)
+        res = ex.exchange_and_step(arena, visible, Adam(list(pb.values()), lr=0.01, eps=1e-15), pb)
+        torch.cuda.synchronize()
+        assert ex.last.collectives == 0 and torch.equal(res.union, visible)
+        for k in LEAF_WIDTHS:
+            assert torch.equal(pa[k].detach(), pb[k].detach()), k
+    finally:
+        dist.destroy_process_group()

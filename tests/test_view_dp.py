@@ -171,3 +171,96 @@ def test_debug_mode_catches_rows_outside_union():
     union = torch.tensor([True, True, False, False, False, False])
     with pytest.raises(RuntimeError, match="outside the visibility union"):
         ex.sum_gradients([g], union=union)
+
+
+class RecordingPlan:
+    """Stands in for hidegs_amd.optim.AdamStepPlan on CPU: records which rows were stepped and what
+    the arena held for them at that moment."""
+
+    def __init__(self, arena, names):
+        self.arena, self.names = arena, names
+        self.calls, self.snap = [], {}
+
+    def run(self):
+        self.calls.append(("all", 0, 0))
+
+    def run_rows(self, p, r0, r1):
+        name = self.names[id(p)]
+        self.calls.append((name, r0, r1))
+        self.snap[(name, r0, r1)] = self.arena[name][r0:r1].clone()
+
+
+class RecordingOptimizer:
+    def __init__(self, plan):
+        self.plan, self.relevant = plan, None
+
+    def begin_step(self, relevant):
+        self.relevant = relevant.clone()
+        return self.plan
+
+
+def worker_step(rank, world, port, compact_below, bucket_bytes, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        visible, grads, norm, _ = rank_inputs(rank, 0)
+        arena = GradArena(N)
+        params = {k: torch.nn.Parameter(torch.zeros(N, w)) for k, w in LEAF_WIDTHS.items()}
+        for k, v in grads.items():
+            arena[k].copy_(v)
+        plan = RecordingPlan(arena, {id(p): k for k, p in params.items()})
+        opt = RecordingOptimizer(plan)
+        ex = ViewDPExchange(bucket_bytes=bucket_bytes, compact_below=compact_below)
+        res = ex.exchange_and_step(arena, visible, opt, params, max_stats=[norm])
+        all_in = [rank_inputs(r, 0) for r in range(world)]
+        exp = {k: sum(a[1][k] for a in all_in) for k in LEAF_WIDTHS}
+        exp_union = torch.zeros(N, dtype=torch.bool)
+        for a in all_in:
+            exp_union |= a[0]
+        ok = torch.equal(res.union, exp_union) and torch.equal(opt.relevant, exp_union)
+        ok = ok and all(torch.allclose(arena[k], exp[k], atol=1e-5) for k in LEAF_WIDTHS)
+        if plan.calls == [("all", 0, 0)]:
+            mode = "whole"
+        else:
+            mode = "rows"
+            # every row of every field stepped exactly once, in order, after its bucket was reduced
+            for k in LEAF_WIDTHS:
+                spans = [(r0, r1) for (name, r0, r1) in plan.calls if name == k]
+                ok = ok and spans[0][0] == 0 and spans[-1][1] == N
+                ok = ok and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            ok = ok and [c[0] for c in plan.calls] == sorted((c[0] for c in plan.calls),
+                                                             key=list(LEAF_WIDTHS).index)
+            for (name, r0, r1), got in plan.snap.items():
+                ok = ok and torch.allclose(got, exp[name][r0:r1], atol=1e-5)
+        if rank == 0:
+            q.put((ok, mode, ex.last.collectives))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_step(world, compact_below, bucket_bytes):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker_step, args=(r, world, port, compact_below, bucket_bytes, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    return q.get(timeout=10)
+
+
+@pytest.mark.parametrize("world,compact_below,bucket_bytes,mode", [
+    (2, 0.0, 4096, "rows"),       # dense: per-bucket steps overlapped with the later buckets' reduces
+    (3, 0.0, 1 << 20, "rows"),
+    (2, 1.0, 4096, "whole"),      # compacted: reduce, then one step
+    (1, 0.0, 4096, "whole"),      # one rank: no collective at all
+])
+def test_exchange_and_step_steps_each_row_once_after_its_reduction(world, compact_below, bucket_bytes, mode):
+    ok, got_mode, collectives = run_step(world, compact_below, bucket_bytes)
+    assert ok and got_mode == mode
+    if world == 1:
+        assert collectives == 0
