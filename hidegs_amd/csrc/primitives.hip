@@ -6,13 +6,15 @@
 //                                  (rasterizer_impl.cu:193-196,354-362; simple_knn.cu:211-214)
 //   hidegs_identify_tile_ranges <- cudaMemsetAsync(ranges) + identifyTileRanges
 //                                  (rasterizer_impl.cu:364-371,120-142)
+//   hidegs_sort_tile_pairs      <- SortPairs + memset + identifyTileRanges as one call
+//                                  (rasterizer_impl.cu:354-371)
 //   hidegs_higher_msb           <- getHigherMsb (rasterizer_impl.cu:35-50)
 //
 // Design (MI355X-first, not a CUB restatement):
 //  * Tiles of 4096 items per 256-thread workgroup (4 x wave64, 16 items per lane),
 //    global traffic in 16-byte-per-lane vector loads where the layout allows.
-//  * Scan: reduce -> scan of tile sums -> rescan, three stream-ordered launches
-//    with no inter-workgroup hand-off inside a launch.
+//  * Scan: tile sums, then a rescan in which each workgroup adds up the sums before it
+//    (two stream-ordered launches, no inter-workgroup hand-off inside a launch).
 //  * Radix sort: LSD, 8-bit digits, per pass three launches:
 //      1. tile histogram  (per-wave LDS histograms, digit-major counts[d][tile])
 //      2. per-digit exclusive scan over tiles (one workgroup per digit)
@@ -38,7 +40,6 @@ constexpr int kItems = HIDEGS_RADIX_ITEMS;
 constexpr int kTile = kBlock * kItems;       // 4096
 constexpr int kWavesPerBlock = kBlock / kWave;  // 4
 constexpr int kRadixBits = 8;
-
 constexpr int kRadix = 1 << kRadixBits;     // 256
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
@@ -354,15 +355,15 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
 // Keys whose bits [32, end_bit) are a small segment id -- the (tile | depth) keys of the
 // binning stage -- are sorted in two stages with the same result as the LSD sort over
 // [0, end_bit): (1) the LSD passes above over [32, end_bit) only, which partition the pairs
-// stably by segment; (2) one workgroup per segment sorts it stably by the low 32 bits in LDS.
+// stably by segment; (2) one workgroup per segment sorts it stably by the low 32 bits.
 // Global traffic drops from 6 LSD passes to 2 plus one read/write of every pair.
 //
-// Stage (2) is latency-bound (a tile holds ~1000 pairs), so the workgroup's LDS is sized for
-// one run of kSegRun pairs (~21 KB, 7 workgroups per CU).  A segment of up to kSegCap pairs
-// is sorted as two runs, the first parked in registers while the second is sorted, and the
-// runs are merged by rank (binary search in LDS).  Larger segments go to a list that a second
-// kernel sorts through global memory.
-
+// Stage (2) has three forms, chosen per segment (block-uniform):
+//   bucket form  (<= kSegCap pairs, the common case): bucket by the top 10 varying low-key bits,
+//                exact rank inside each bucket, LDS-staged in-place stores -- see segment_sort_kernel;
+//   LSD form     (a bucket over kMaxBucket pairs: crowded depths): 8-bit LDS LSD passes over the
+//                varying bits, two runs of <= kSegRun merged by rank;
+//   global form  (> kSegCap pairs: a hot tile): 4 LSD passes through global memory.
 #ifndef HIDEGS_SEG_BITS
 #define HIDEGS_SEG_BITS 32  // experiments only (tools/build_variant.py): fewer bits give wrong orders
 #endif
@@ -864,6 +865,9 @@ size_t scan_scratch(long long n)
 
 constexpr int kMaxSegmentBits = 16;        // segmented path: at most 65536 segments
 constexpr long long kSegmentedMinN = 65536;  // below this the plain LSD passes are cheaper
+constexpr long long kSegmentedMinAvg = 64;   // pairs per segment on average, else the plain passes: one
+                                             // workgroup per ~30-pair segment (distCUDA2's 48-bit Morton
+                                             // keys of 2M points) costs more than the 4 low-digit passes
 
 template <typename K>
 size_t sort_scratch(long long n)
@@ -918,7 +922,7 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
 
     // (tile | depth)-shaped sort: LSD over the segment bits only, then per-segment LDS sorts
     const bool segmented = sizeof(K) == 8 && begin_bit == 0 && end_bit > 32 && end_bit - 32 <= kMaxSegmentBits &&
-                           n >= kSegmentedMinN;
+                           n >= kSegmentedMinN && n >= (kSegmentedMinAvg << (end_bit - 32));
     const int lo_bit = segmented ? 32 : begin_bit;
     const int lsd_passes = segmented ? (end_bit - 32 + kRadixBits - 1) / kRadixBits : passes;
 
