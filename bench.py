@@ -27,7 +27,9 @@ on (config 3: 2M Gaussians, one 1920x1080 view, synthetic D2 inputs resident in 
               drop-in) over the six HiDeGS parameter groups at 2M Gaussians (59 fp32 each), 90%
               of rows visible; 28 algorithmic bytes per updated value; beside it the reference's
               own op sequence (OurAdam.py:249-337 restated as torch ops) on the same GPU.
-  cpu_baseline = the oracle's stable sort (numpy, one core) on the same 8M pairs.
+  cpu_baseline = the oracle's stable sort (numpy, one core) on the same 8M pairs; beside the
+              distCUDA2 and masked Adam lines, the oracle's brute force on a sample of queries and
+              its masked Adam step.
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -304,6 +306,39 @@ def main() -> None:
                                 "sample": f"stable sort of the same {K} (key, value) pairs over bits [0,{end_bit}) "
                                           f"(numpy argsort kind=stable + gather, oracle/binning.py), {reps} reps",
                                 "cpu": cpu_model(), "gpu_speedup_sort": round(dt * 1e3 / (sort_us * 1e-3), 1)}
+        import oracle
+        omp = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+        # distCUDA2: the oracle's brute force (OpenMP) for a sample of the 2M D2 queries, each
+        # against all 2M points
+        if "distCUDA2" in line:
+            cpu_pts = synthetic.frustum_points(N_GAUSSIANS, seed=rank).numpy()
+            nq = 256
+            idx = np.random.default_rng(0).choice(N_GAUSSIANS, nq, replace=False)
+            t0 = time.perf_counter()
+            oracle.knn_mean3_subset(cpu_pts, idx)
+            dq = time.perf_counter() - t0
+            line["distCUDA2"]["cpu_baseline"] = {
+                "value": nq / dq, "unit": "queries/s", "cores": omp, "kind": "port",
+                "sample": f"{nq} of the {N_GAUSSIANS} D2 queries, each brute-forced against all points "
+                          "(oracle/knn_ref.c, OpenMP)",
+                "gpu_queries_per_s": line["distCUDA2"]["points_per_s_all_ranks"]}
+            del cpu_pts
+        # masked Adam: the oracle's restatement (oracle/adam_ref.c, one core) of one step over the
+        # same six 2M-row parameter groups, 90% of rows relevant
+        if "masked_adam" in line:
+            rng = np.random.default_rng(1)
+            rel = rng.random(N_GAUSSIANS) < 0.9
+            t_total = 0.0
+            for w in (3, 3, 45, 1, 3, 4):
+                pa = rng.standard_normal((N_GAUSSIANS, w), dtype=np.float32)
+                ga = rng.standard_normal((N_GAUSSIANS, w), dtype=np.float32)
+                ma, va = np.zeros_like(pa), np.zeros_like(pa)
+                t0 = time.perf_counter()
+                oracle.masked_adam(pa, ga, ma, va, rel, 1e-3, 0.9, 0.999, 1e-15, 0.0, 1)
+                t_total += time.perf_counter() - t0
+            line["masked_adam"]["cpu_baseline"] = {
+                "value": 1e3 * t_total, "unit": "ms per step", "cores": 1, "kind": "port",
+                "sample": f"one full step, {N_GAUSSIANS} Gaussians x 59 floats, 90% of rows relevant"}
 
     dist.destroy_process_group()
     sys.stdout.flush()

@@ -1,4 +1,4 @@
-"""Generates the committed distCUDA2 fixtures in tests/golden/.
+"""Generates the committed fixtures in tests/golden/.
 
 knn_kat.json   hand-checkable known answers, each derived from distCUDA2's definition in
                the reference text (submodules/simple-knn/simple_knn.cu:133-184): three best
@@ -8,6 +8,13 @@ knn_kat.json   hand-checkable known answers, each derived from distCUDA2's defin
                C oracle, and the CPU tests check the oracle against them.
 knn_random.npz seeded point sets and the oracle's (oracle/knn_ref.c) values for them; the
                GPU tests compare the HIP kernels with these and with the live oracle.
+binning.npz    binning sort + tile-range cases (SortPairs over [0, 32 + getHigherMsb(T)),
+               identifyTileRanges; rasterizer_impl.cu:35-50,120-142,354-371): raster-like
+               (tile << 32 | float depth bits, Gaussian-major ids) inputs and the expected
+               permutation and ranges, computed by plain Python sorting on the tuple
+               (tile, depth bits, input index) -- the definition of a stable sort over those
+               bits -- and cross-checked against oracle/binning.py.  One case is large enough
+               (66,000 pairs) for the segmented GPU path.
 
 Run from the repository root:  python tests/golden/make_golden.py
 """
@@ -98,7 +105,61 @@ def make_random():
     np.savez_compressed(os.path.join(HERE, "knn_random.npz"), **arrays)
 
 
+def binning_cases(seed=11):
+    g = np.random.default_rng(seed)
+    cases = {}
+    # config-1 shape: 64 tiles, Gaussian-major emission, depths in [2, 20]
+    def raster(n_gauss, tiles, spread):
+        tl, dp = [], []
+        for _ in range(n_gauss):
+            t0 = int(g.integers(0, tiles))
+            z = np.float32(g.uniform(2.0, 20.0))
+            for k in range(int(g.integers(1, spread + 1))):
+                tl.append((t0 + k) % tiles)
+                dp.append(z)
+        return np.array(tl, np.uint16), np.array(dp, np.float32).view(np.uint32)
+    cases["config1_64_tiles"] = (*raster(256, 64, 4), 64)
+    t, d = raster(400, 10, 3)
+    d[::3] = d[0]  # equal depths: stability shows
+    cases["ties_10_tiles"] = (t, d, 10)
+    cases["one_pair"] = (np.array([5], np.uint16), np.array([np.float32(3.5).view(np.uint32)], np.uint32), 8)
+    # segmented path (>= 65536 pairs, >= 64 per segment): 256 tiles, crowded depth buckets
+    t = g.integers(0, 256, 66_000).astype(np.uint16)
+    d = g.uniform(0.5, 60.0, 66_000).astype(np.float32).view(np.uint32)
+    d[::4] = (np.float32(7.0).view(np.uint32) & 0xFFFFF000) | g.integers(0, 4096, d[::4].size).astype(np.uint32)
+    cases["segmented_256_tiles"] = (t, d, 256)
+    return cases
+
+
+def make_binning():
+    from oracle import binning
+    arrays = {}
+    for name, (tiles, depth, T) in binning_cases().items():
+        n = tiles.size
+        keys = (tiles.astype(np.uint64) << np.uint64(32)) | depth.astype(np.uint64)
+        vals = np.arange(n, dtype=np.uint32)
+        perm = np.array(sorted(range(n), key=lambda i: (int(tiles[i]), int(depth[i]), i)), dtype=np.uint32)
+        ranges = np.zeros((T, 2), np.uint32)
+        for pos, i in enumerate(perm):
+            t = int(tiles[i])
+            if ranges[t, 1] == 0 and (pos == 0 or int(tiles[perm[pos - 1]]) != t):
+                ranges[t, 0] = pos
+            ranges[t, 1] = pos + 1
+        if n == 1:
+            ranges[int(tiles[0]), 1] = 0  # identifyTileRanges' single-key edge
+        end = 32 + max(1, T.bit_length())
+        ek, ev = binning.stable_sort_pairs(keys, vals, 0, end)
+        assert np.array_equal(ev, perm) and np.array_equal(binning.tile_ranges(ek, T), ranges), name
+        arrays[name + "__tiles"] = tiles
+        arrays[name + "__depth_bits"] = depth
+        arrays[name + "__num_tiles"] = np.array([T], np.int64)
+        arrays[name + "__perm"] = perm
+        arrays[name + "__ranges"] = ranges
+    np.savez_compressed(os.path.join(HERE, "binning.npz"), **arrays)
+
+
 if __name__ == "__main__":
     make_kat()
     make_random()
+    make_binning()
     print("wrote", os.listdir(HERE))

@@ -203,3 +203,21 @@ def test_sort_tile_pairs_equals_sort_then_ranges(K, T):
     assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
     assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
     assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
+
+
+def test_sort_and_tile_ranges_match_committed_fixture():
+    """tests/golden/binning.npz (plain-Python expected permutations and ranges, one case on the
+    segmented path): sort_pairs + identify_tile_ranges and sort_tile_pairs reproduce them."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "binning.npz"))
+    for name in sorted({k.split("__")[0] for k in z.files}):
+        tiles, depth = z[name + "__tiles"], z[name + "__depth_bits"]
+        T = int(z[name + "__num_tiles"][0])
+        keys = (tiles.astype(np.uint64) << np.uint64(32)) | depth.astype(np.uint64)
+        vals = np.arange(keys.size, dtype=np.uint32)
+        ko, vo = primitives.sort_pairs(u64(keys), u32(vals), 0, 32 + primitives.higher_msb(T))
+        r = primitives.identify_tile_ranges(ko, T)
+        assert np.array_equal(vo.cpu().numpy().view(np.uint32), z[name + "__perm"]), name
+        assert np.array_equal(r.cpu().numpy().view(np.uint32), z[name + "__ranges"]), name
+        ko2, vo2, r2 = primitives.sort_tile_pairs(u64(keys), u32(vals), T)
+        assert torch.equal(ko2, ko) and torch.equal(vo2, vo) and torch.equal(r2, r), name

@@ -93,3 +93,25 @@ def test_stable_sort_oracle_is_stable_over_bit_range():
 def test_scan_oracle_wraps():
     x = np.array([0xFFFFFFFF, 2, 3], dtype=np.uint32)
     assert binning.inclusive_scan_u32(x).tolist() == [0xFFFFFFFF, 1, 4]
+
+
+def binning_fixture():
+    z = np.load(os.path.join(GOLD, "binning.npz"))
+    names = sorted({k.split("__")[0] for k in z.files})
+    out = {}
+    for name in names:
+        tiles, depth = z[name + "__tiles"], z[name + "__depth_bits"]
+        keys = (tiles.astype(np.uint64) << np.uint64(32)) | depth.astype(np.uint64)
+        out[name] = (keys, int(z[name + "__num_tiles"][0]), z[name + "__perm"], z[name + "__ranges"])
+    return out
+
+
+@pytest.mark.parametrize("name", sorted(binning_fixture()))
+def test_binning_oracle_matches_committed_fixture(name):
+    """tests/golden/binning.npz: expected permutation and ranges from plain Python sorting on
+    (tile, depth bits, index) -- the oracle must agree."""
+    keys, T, perm, ranges = binning_fixture()[name]
+    vals = np.arange(keys.size, dtype=np.uint32)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + binning.bit_length_at_least_one(T))
+    assert np.array_equal(ev, perm)
+    assert np.array_equal(binning.tile_ranges(ek, T), ranges)
