@@ -319,8 +319,14 @@ __global__ __launch_bounds__(kBlock) void super_box_kernel(const Box* __restrict
 #define HIDEGS_KNN_GROUPS 2
 #endif
 constexpr int kGroups = HIDEGS_KNN_GROUPS;  // query groups per wave for the coarse filter
-constexpr int kSuperBatch = 4;              // super-boxes tested per lane per batch
-constexpr int kLeafBatch = 4;               // passing super-boxes whose leaf boxes load together
+#ifndef HIDEGS_KNN_SUPER_BATCH
+#define HIDEGS_KNN_SUPER_BATCH 2
+#endif
+#ifndef HIDEGS_KNN_LEAF_BATCH
+#define HIDEGS_KNN_LEAF_BATCH 2
+#endif
+constexpr int kSuperBatch = HIDEGS_KNN_SUPER_BATCH;  // super-boxes tested per lane per batch
+constexpr int kLeafBatch = HIDEGS_KNN_LEAF_BATCH;    // passing super-boxes whose leaf boxes load together
 constexpr int kListCap = 256;               // candidate leaves buffered per wave
 #ifndef HIDEGS_KNN_FLUSH_BATCH
 #define HIDEGS_KNN_FLUSH_BATCH 4
@@ -382,7 +388,10 @@ struct KnnCounters {
     uint32_t hist[8];           // waves by coarse leaves: <16, <32, <64, <128, <256, <512, <1024, more
 };
 
-__global__ __launch_bounds__(kBlock) void knn_leaf_kernel(const float4* __restrict__ sp, int P, int nleaves, int nsuper,
+#ifndef HIDEGS_KNN_WAVES
+#define HIDEGS_KNN_WAVES 5  // waves per SIMD the phase-1 register budget is set for (91 VGPRs, no spills)
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_KNN_WAVES))) void knn_leaf_kernel(const float4* __restrict__ sp, int P, int nleaves, int nsuper,
                                                           const Box* __restrict__ leaves, const Box* __restrict__ subs,
                                                           const Box* __restrict__ supers,
                                                           float* __restrict__ out, uint32_t* __restrict__ hard,
