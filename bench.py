@@ -19,6 +19,7 @@ on (config 3: 2M Gaussians, one 1920x1080 view, synthetic D2 inputs resident in 
               over its launches with per-launch HIP events (hidegs_kernel_timing), against
               8 TB/s; traffic from the committed rocprofv3 PMC summary when present.
   distCUDA2 = simple_knn._C.distCUDA2 on the 2M D2 centres (once-per-scene initialiser).
+  config5_scale = the same binning step and distCUDA2 at config 5's size (10M Gaussians, 4K frame).
   exchange  = the view-DP exchange of 2M x 59 fp32 leaf gradients + stats over RCCL
               (a one-rank group at N = 1), HIP-event timed.
   exchange_and_step = the exchange followed by the masked step, in sequence and overlapped bucket
@@ -78,6 +79,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exchange", action="store_true")
     ap.add_argument("--no-adam", action="store_true")
+    ap.add_argument("--no-config5", action="store_true")
     args = ap.parse_args()
 
     # The contract is ONE JSON line on stdout; RCCL prints a version banner there at init, so the
@@ -214,6 +216,25 @@ def main() -> None:
                          "points_per_s_all_ranks": N_GAUSSIANS * world / (knn_ms * 1e-3), "kernels_us": kk,
                          "algorithmic_bytes": 16 * N_GAUSSIANS,
                          "hbm_frac": round(16 * N_GAUSSIANS / (knn_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
+
+    # ---- config 5's scale: 10M Gaussians, 3840x2160 frame ------------------------------------
+    if not args.no_config5:
+        wl5 = synthetic.binning_workload(10_000_000, 3840, 2160, seed=rank, device=dev)
+        off5 = torch.empty_like(wl5.tiles_touched)
+
+        def step5():
+            primitives.inclusive_scan_u32(wl5.tiles_touched, out=off5)
+            primitives.sort_tile_pairs(wl5.keys, wl5.values, wl5.num_tiles)
+
+        ms5, _ = timed(step5, 20, 3)
+        pts5 = synthetic.frustum_points(10_000_000, seed=rank).to(dev)
+        knn5_ms, _ = timed(lambda: simple_knn._C.distCUDA2(pts5), 3, 1)
+        line["config5_scale"] = {"workload": "10M Gaussians, 3840x2160 (32400 tiles): binning step and distCUDA2",
+                                 "binning_ms_per_step": round(ms5, 4), "pairs_K": wl5.num_pairs,
+                                 "sort_bits": [0, 32 + primitives.higher_msb(wl5.num_tiles)],
+                                 "pairs_per_s_all_ranks": wl5.num_pairs * world / (ms5 * 1e-3),
+                                 "distCUDA2_ms": round(knn5_ms, 3)}
+        del wl5, off5, pts5
 
     # ---- view-DP exchange at 2M ---------------------------------------------------------------
     if not args.no_exchange:

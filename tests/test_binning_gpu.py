@@ -221,3 +221,18 @@ def test_sort_and_tile_ranges_match_committed_fixture():
         assert np.array_equal(r.cpu().numpy().view(np.uint32), z[name + "__ranges"]), name
         ko2, vo2, r2 = primitives.sort_tile_pairs(u64(keys), u32(vals), T)
         assert torch.equal(ko2, ko) and torch.equal(vo2, vo) and torch.equal(r2, r), name
+
+
+def test_config5_scale_4k_frame_sort_tile_pairs():
+    """Config 5's binning shape: 10M Gaussians on a 3840x2160 frame (32,400 tiles, sort over
+    [0, 47)), K ~ 40M pairs through hidegs_sort_tile_pairs, bit-identical to the oracle."""
+    from hidegs_amd import synthetic
+    wl = synthetic.binning_workload(10_000_000, 3840, 2160, seed=8, device="cuda")
+    assert wl.num_tiles == 32400
+    ko, vo, r = primitives.sort_tile_pairs(wl.keys, wl.values, wl.num_tiles)
+    keys, vals = wl.keys.cpu().numpy().view(np.uint64), wl.values.cpu().numpy().view(np.uint32)
+    del wl
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(32400))
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, 32400))

@@ -136,3 +136,13 @@ def test_runs_on_current_stream_and_device_tensor_types():
     # non-contiguous input is made contiguous like the reference's points.contiguous()
     wide = torch.rand(5000, 6, device="cuda")
     assert torch.equal(simple_knn._C.distCUDA2(wide[:, ::2]), simple_knn._C.distCUDA2(wide[:, ::2].contiguous()))
+
+
+def test_config5_scale_10m_sampled(oracle_lib):
+    """Config 5's scene size (10M points): sampled queries bit-exact against the brute-force oracle
+    (each against all 10M points), and the result is finite and non-negative everywhere."""
+    pts = frustum_points(10_000_000, seed=4)
+    got = knn(pts)
+    assert got.shape == (10_000_000,) and np.isfinite(got).all() and (got >= 0).all()
+    idx = np.random.default_rng(10).choice(len(pts), 256, replace=False)
+    assert_bits_equal(got[idx], oracle_lib.knn_mean3_subset(pts, idx), "frustum 10M sample")
