@@ -57,6 +57,6 @@ int hidegs_mark_visible(int, const float*, const float*, const float*, unsigned 
 }
 
 const char* hidegs_last_error(void) { return hidegs::last_error().c_str(); }
-const char* hidegs_version(void) { return "hidegs-abi 0.3 (gfx950: distCUDA2, scan, radix sort, tile ranges)"; }
+const char* hidegs_version(void) { return "hidegs-abi 0.4 (gfx950: distCUDA2, scan, radix sort, tile sort + ranges, masked Adam)"; }
 
 }  // extern "C"
