@@ -278,6 +278,7 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
     __shared__ __attribute__((aligned(16))) K s_stage[kTile];  // keys by tile-local rank, then values
     __shared__ uint32_t s_cnt[kWavesPerBlock][kRadix];  // per-wave running counters, later global offsets
     __shared__ uint32_t s_start[kRadix];                // tile-local start of each digit run
+    __shared__ uint32_t s_off[kRadix];                  // global position of tile-local position 0 of digit d
     __shared__ uint32_t s_wave[kWavesPerBlock];
     uint32_t* s_vals = reinterpret_cast<uint32_t*>(s_stage);
 
@@ -301,15 +302,19 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
         k[r] = ok[r] ? keys_in[i] : K(0);
         v[r] = ok[r] ? vals_in[i] : 0u;
     }
-    __syncthreads();
+    // the digits' global bases, scanned while the tile's loads are in flight (workgroup barriers
+    // do not wait for global loads)
+    uint32_t dummy;
+    const uint32_t digit_base = block_exclusive_scan(digit_total, s_wave, &dummy) + digit_prefix;
     uint32_t rank[kItems];
     wave_rank<K, kItems>(k, ok, shift, mask, s_cnt[wave], rank, mask);
     __syncthreads();
 
     const int d = t;
     const uint32_t tile_count_d = digit_wave_prefix(s_cnt);
-    uint32_t dummy;
-    s_start[d] = block_exclusive_scan(tile_count_d, s_wave, &dummy);
+    const uint32_t start_d = block_exclusive_scan(tile_count_d, s_wave, &dummy);
+    s_start[d] = start_d;
+    s_off[d] = digit_base - start_d;
     __syncthreads();
     uint32_t pos[kItems];
 #pragma unroll
@@ -321,11 +326,6 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
         }
     }
     __syncthreads();
-    {
-        const uint32_t dbase = block_exclusive_scan(digit_total, s_wave, &dummy);
-        s_cnt[0][d] = dbase + digit_prefix - s_start[d];
-    }
-    __syncthreads();
     const int count = (int)((n - base) < kTile ? (n - base) : kTile);
     uint32_t dst[kItems];
 #pragma unroll
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
         dst[j] = 0xffffffffu;
         if (i < count) {
             const K key = s_stage[i];
-            dst[j] = s_cnt[0][digit_of(key, shift, mask)] + i;
+            dst[j] = s_off[digit_of(key, shift, mask)] + i;
             if (dst[j] < n) keys_out[dst[j]] = key;  // always true for consistent counts
         }
     }
@@ -517,8 +517,10 @@ __device__ __forceinline__ void segment_sort_global(uint64_t* __restrict__ keys,
                 if (ok[q]) {
                     const uint32_t dd = digit_of(k[q], shift, kRadix - 1);
                     const uint32_t dst = sh.run[dd] + sh.cnt[wave][dd] + rank[q];
-                    dk[dst] = k[q];
-                    dv[dst] = v[q];
+                    if (dst < begin + m) {  // always, for a consistent segment; never outside it
+                        dk[dst] = k[q];
+                        dv[dst] = v[q];
+                    }
                 }
             }
             __syncthreads();
