@@ -11,8 +11,9 @@ constexpr int kScanWaves = kScanBlock / kWave;  // 4
 constexpr int kScanItems = 16;
 constexpr int kScanTile = kScanBlock * kScanItems;  // 4096
 
-// Block-wide exclusive scan of one u32 per thread (256 threads); returns the
-// exclusive prefix and writes the block total to *total.
+// Block-wide exclusive scan of one u32 per thread (W wave64s, 256 threads by default); returns
+// the exclusive prefix and writes the block total to *total.  s_wave holds W entries.
+template <int W = kScanWaves>
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t* total)
 {
     const int lane = lane_id();
@@ -22,7 +23,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
     __syncthreads();
     uint32_t woff = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < kScanWaves; w++) {
+    for (int w = 0; w < W; w++) {
         uint32_t s = s_wave[w];
         if (w < wave) woff += s;
         tot += s;

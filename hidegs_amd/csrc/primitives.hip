@@ -263,40 +263,51 @@ __global__ __launch_bounds__(kBlock) void radix_digit_scan_kernel(uint32_t* __re
 }
 
 // Stable scatter of one tile.  LDS: one staging buffer of the tile's keys (values reuse it
-// afterwards), per-wave digit counters -- 37 KB, so 4 workgroups fit a CU.
+// afterwards), per-wave digit counters -- 43 KB at 8 waves, 3 workgroups per CU.
 // Global offsets: tile_prefix[d][tile] (per-digit exclusive scan over tiles) + exclusive scan
 // of the digit totals.  (A single-pass decoupled look-back variant measured slower on MI355X:
 // the chained tile-to-tile hand-off crosses the non-coherent per-XCD L2s at every hop.)
+#ifndef HIDEGS_SCATTER_WAVES
+#define HIDEGS_SCATTER_WAVES 8  // wave64s per scatter workgroup (the tile stays kTile pairs); 8 waves
+                                // of 8 pairs each (66 VGPRs, 6 waves/SIMD) measured 2-3% faster than 4 of 16
+#endif
+constexpr int kSWaves = HIDEGS_SCATTER_WAVES;
+constexpr int kSBlock = kSWaves * kWave;
+constexpr int kSItems = kTile / kSBlock;  // pairs per thread
+static_assert(kSBlock >= kRadix, "one thread per digit in the digit scans");
+
 template <typename K>
-__global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restrict__ keys_in,
-                                                               const uint32_t* __restrict__ vals_in,
-                                                               K* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                               long long n, int shift, uint32_t mask, int ntiles,
-                                                               const uint32_t* __restrict__ tile_prefix,
-                                                               const uint32_t* __restrict__ totals)
+__global__ __launch_bounds__(kSBlock) void radix_scatter_kernel(const K* __restrict__ keys_in,
+                                                                const uint32_t* __restrict__ vals_in,
+                                                                K* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+                                                                long long n, int shift, uint32_t mask, int ntiles,
+                                                                const uint32_t* __restrict__ tile_prefix,
+                                                                const uint32_t* __restrict__ totals)
 {
     __shared__ __attribute__((aligned(16))) K s_stage[kTile];  // keys by tile-local rank, then values
-    __shared__ uint32_t s_cnt[kWavesPerBlock][kRadix];  // per-wave running counters, later global offsets
+    __shared__ uint32_t s_cnt[kSWaves][kRadix];         // per-wave running counters
     __shared__ uint32_t s_start[kRadix];                // tile-local start of each digit run
     __shared__ uint32_t s_off[kRadix];                  // global position of tile-local position 0 of digit d
-    __shared__ uint32_t s_wave[kWavesPerBlock];
+    __shared__ uint32_t s_wave[kSWaves];
     uint32_t* s_vals = reinterpret_cast<uint32_t*>(s_stage);
 
     const int t = threadIdx.x;
     const int lane = lane_id();
     const int wave = t / kWave;
-    for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&s_cnt[0][0])[i] = 0;
+    const bool digit_thread = t < kRadix;  // thread d owns digit d in the digit scans
+    for (int i = t; i < kSWaves * kRadix; i += kSBlock) (&s_cnt[0][0])[i] = 0;
     const long long base = (long long)blockIdx.x * kTile;
-    const long long seg = base + (long long)wave * (kItems * kWave);  // this wave's items
+    const long long seg = base + (long long)wave * (kSItems * kWave);  // this wave's items
     // this tile's global digit offsets, loaded now so their latency hides behind the ranking (digits
     // above `mask` read stale counts that no item uses)
-    const uint32_t digit_total = totals[t], digit_prefix = tile_prefix[(long long)t * ntiles + blockIdx.x];
+    const uint32_t digit_total = digit_thread ? totals[t] : 0u;
+    const uint32_t digit_prefix = digit_thread ? tile_prefix[(long long)t * ntiles + blockIdx.x] : 0u;
 
-    K k[kItems];
-    uint32_t v[kItems];
-    bool ok[kItems];
+    K k[kSItems];
+    uint32_t v[kSItems];
+    bool ok[kSItems];
 #pragma unroll
-    for (int r = 0; r < kItems; r++) {
+    for (int r = 0; r < kSItems; r++) {
         const long long i = seg + r * kWave + lane;
         ok[r] = i < n;
         k[r] = ok[r] ? keys_in[i] : K(0);
@@ -305,20 +316,29 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
     // the digits' global bases, scanned while the tile's loads are in flight (workgroup barriers
     // do not wait for global loads)
     uint32_t dummy;
-    const uint32_t digit_base = block_exclusive_scan(digit_total, s_wave, &dummy) + digit_prefix;
-    uint32_t rank[kItems];
-    wave_rank<K, kItems>(k, ok, shift, mask, s_cnt[wave], rank, mask);
+    const uint32_t digit_base = block_exclusive_scan<kSWaves>(digit_total, s_wave, &dummy) + digit_prefix;
+    uint32_t rank[kSItems];
+    wave_rank<K, kSItems>(k, ok, shift, mask, s_cnt[wave], rank, mask);
     __syncthreads();
 
-    const int d = t;
-    const uint32_t tile_count_d = digit_wave_prefix(s_cnt);
-    const uint32_t start_d = block_exclusive_scan(tile_count_d, s_wave, &dummy);
-    s_start[d] = start_d;
-    s_off[d] = digit_base - start_d;
-    __syncthreads();
-    uint32_t pos[kItems];
+    uint32_t tile_count_d = 0;  // thread d: count of digit d in waves before each wave, in place
+    if (digit_thread) {
 #pragma unroll
-    for (int r = 0; r < kItems; r++) {
+        for (int w = 0; w < kSWaves; w++) {
+            const uint32_t c = s_cnt[w][t];
+            s_cnt[w][t] = tile_count_d;
+            tile_count_d += c;
+        }
+    }
+    const uint32_t start_d = block_exclusive_scan<kSWaves>(tile_count_d, s_wave, &dummy);
+    if (digit_thread) {
+        s_start[t] = start_d;
+        s_off[t] = digit_base - start_d;
+    }
+    __syncthreads();
+    uint32_t pos[kSItems];
+#pragma unroll
+    for (int r = 0; r < kSItems; r++) {
         if (ok[r]) {
             const uint32_t dd = digit_of(k[r], shift, mask);
             pos[r] = s_start[dd] + s_cnt[wave][dd] + rank[r];
@@ -327,10 +347,10 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
     }
     __syncthreads();
     const int count = (int)((n - base) < kTile ? (n - base) : kTile);
-    uint32_t dst[kItems];
+    uint32_t dst[kSItems];
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {  // keys, run-contiguous: position i = t + 256 j
-        const int i = t + j * kBlock;
+    for (int j = 0; j < kSItems; j++) {  // keys, run-contiguous: position i = t + kSBlock j
+        const int i = t + j * kSBlock;
         dst[j] = 0xffffffffu;
         if (i < count) {
             const K key = s_stage[i];
@@ -340,12 +360,12 @@ __global__ __launch_bounds__(kBlock) void radix_scatter_kernel(const K* __restri
     }
     __syncthreads();  // every key read: the staging buffer takes the values
 #pragma unroll
-    for (int r = 0; r < kItems; r++)
+    for (int r = 0; r < kSItems; r++)
         if (ok[r]) s_vals[pos[r]] = v[r];
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
-        const int i = t + j * kBlock;
+    for (int j = 0; j < kSItems; j++) {
+        const int i = t + j * kSBlock;
         if (i < count && dst[j] < n) vals_out[dst[j]] = s_vals[i];
     }
 }
@@ -947,7 +967,7 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         HIDEGS_LAUNCH("radix_digit_scan", radix_digit_scan_kernel, dim3(mask + 1), dim3(kBlock), 0, stream, counts,
                       nt, totals);
         HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"), radix_scatter_kernel<K>,
-                      dim3(nt), dim3(kBlock), 0, stream, src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals);
+                      dim3(nt), dim3(kSBlock), 0, stream, src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals);
         src_k = dk;
         src_v = dv;
         shift += bits;
