@@ -169,7 +169,10 @@ def main() -> None:
     traffic = None
     rocprof_name = {"radix_scatter_u64": "radix_scatter_kernel", "segment_sort": "segment_sort_kernel",
                     "radix_hist_u64": "radix_hist_kernel"}.get(dom, dom + "_kernel")
-    grid = {"segment_sort": T * 256}.get(dom, ((K + 4095) // 4096) * 256)
+    # launch grid (threads) the rocprof summary keys the kernel by: one workgroup per tile (T) or per
+    # 4096-pair tile of the sort (the scatter runs 512-thread workgroups, the others 256)
+    ntiles_sort = (K + 4095) // 4096
+    grid = {"segment_sort": T * 256, "radix_scatter_u64": ntiles_sort * 512}.get(dom, ntiles_sort * 256)
     if os.path.exists(TRAFFIC_FILE):
         with open(TRAFFIC_FILE) as f:
             traffic = json.load(f).get(f"{rocprof_name}@{grid}", {}).get("hbm_bytes_per_launch")
