@@ -481,25 +481,79 @@ __device__ __forceinline__ void wave_and_or(uint32_t& a, uint32_t& o)
     }
 }
 
-// LDS of the oversized-segment form.
+// LDS of the oversized-segment forms (the one-workgroup global form, the partition jobs).
 struct BigShared {
     uint32_t cnt[kWavesPerBlock][kRadix];
     uint32_t hist[kRadix];
-    uint32_t run[kRadix];  // running start of each digit within the segment
+    uint32_t run[kRadix];  // running destination of each digit
+    uint32_t aux[2][kRadix];  // partition jobs: AND / OR of each digit's low key halves
     uint32_t wave[kWavesPerBlock];
 };
 
-// A segment of more than kSegCap pairs (a hot tile): 4 stable LSD passes over the low 32 bits
-// through global memory (keys/vals <-> alt within the segment's range), 2048 items per step (8 per
-// thread keeps the kernel inside the bucket form's register budget), by the segment's own workgroup.
+// One stable step of a digit pass through global memory: the cnt <= kBigItems * kBlock items
+// [base, base + cnt) of (sk, sv) are ranked by digit (key >> shift) & mask inside the step (wave w
+// owns items [w * 512, w * 512 + 512) in (round, lane) order) and item i goes to
+// sh.run[digit] + its rank, then sh.run advances by the step's digit counts.  sh.run must be set
+// before the call (its first barrier publishes it).  Destinations outside [lo, hi) are dropped:
+// never, for consistent offsets -- a guard, not a case.
 constexpr int kBigItems = 8;
+constexpr int kBigStep = kBigItems * kBlock;  // 2048
+// Track: also fold each item's low key half into sh.aux[0][digit] (AND) and sh.aux[1][digit] (OR).
+template <bool Track = false>
+__device__ __forceinline__ void scatter_step(const uint64_t* sk, const uint32_t* sv, uint64_t* dk, uint32_t* dv,
+                                             const uint32_t base, const uint32_t cnt, const int shift,
+                                             const uint32_t mask, const uint32_t lo, const uint32_t hi,
+                                             BigShared& sh)
+{
+    const int t = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = t / kWave;
+    for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&sh.cnt[0][0])[i] = 0;
+    __syncthreads();
+    uint64_t k[kBigItems];
+    uint32_t v[kBigItems];
+    bool ok[kBigItems];
+    uint32_t rank[kBigItems];
+    const uint32_t w0 = wave * (kBigItems * kWave);
+#pragma unroll
+    for (int q = 0; q < kBigItems; q++) {
+        const uint32_t i = w0 + q * kWave + lane;
+        ok[q] = i < cnt;
+        k[q] = ok[q] ? sk[base + i] : 0ull;
+        v[q] = ok[q] ? sv[base + i] : 0u;
+    }
+    wave_rank<uint64_t, kBigItems>(k, ok, shift, mask, sh.cnt[wave], rank, mask);
+    __syncthreads();
+    const uint32_t tot = digit_wave_prefix(sh.cnt);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kBigItems; q++) {
+        if (ok[q]) {
+            const uint32_t dd = digit_of(k[q], shift, mask);
+            const uint32_t dst = sh.run[dd] + sh.cnt[wave][dd] + rank[q];
+            if (dst >= lo && dst < hi) {
+                dk[dst] = k[q];
+                dv[dst] = v[q];
+            }
+            if (Track) {
+                atomicAnd(&sh.aux[0][dd], (uint32_t)k[q]);
+                atomicOr(&sh.aux[1][dd], (uint32_t)k[q]);
+            }
+        }
+    }
+    __syncthreads();
+    sh.run[threadIdx.x] += tot;
+    __syncthreads();
+}
+
+// A segment of more than kSegCap pairs sorted by ONE workgroup: 4 stable LSD passes over the low
+// 32 bits through global memory (keys/vals <-> alt within the segment's range).  The last resort
+// of the partition queue below (its capacity exhausted); hot tiles normally go through the queue.
 __device__ __forceinline__ void segment_sort_global(uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                     uint64_t* __restrict__ alt_k, uint32_t* __restrict__ alt_v,
                                                     const uint32_t begin, const uint32_t m, BigShared& sh)
 {
     const int t = threadIdx.x;
-    const int lane = lane_id();
-    const int wave = t / kWave;
     for (int pass = 0; pass < 4; pass++) {
         const int shift = pass * kRadixBits;
         const uint64_t* sk = (pass & 1) ? alt_k : keys;
@@ -512,41 +566,9 @@ __device__ __forceinline__ void segment_sort_global(uint64_t* __restrict__ keys,
         __syncthreads();
         uint32_t dummy;
         sh.run[t] = begin + block_exclusive_scan(sh.hist[t], sh.wave, &dummy);
-        __syncthreads();
-        for (uint32_t c0 = 0; c0 < m; c0 += (kBigItems * kBlock)) {
-            for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&sh.cnt[0][0])[i] = 0;
-            __syncthreads();
-            uint64_t k[kBigItems];
-            uint32_t v[kBigItems];
-            bool ok[kBigItems];
-            uint32_t rank[kBigItems];
-            const uint32_t w0 = c0 + wave * (kBigItems * kWave);
-#pragma unroll
-            for (int q = 0; q < kBigItems; q++) {
-                const uint32_t i = w0 + q * kWave + lane;
-                ok[q] = i < m;
-                k[q] = ok[q] ? sk[begin + i] : 0ull;
-                v[q] = ok[q] ? sv[begin + i] : 0u;
-            }
-            wave_rank<uint64_t, kBigItems>(k, ok, shift, kRadix - 1, sh.cnt[wave], rank, kRadix - 1);
-            __syncthreads();
-            const uint32_t tot = digit_wave_prefix(sh.cnt);
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < kBigItems; q++) {
-                if (ok[q]) {
-                    const uint32_t dd = digit_of(k[q], shift, kRadix - 1);
-                    const uint32_t dst = sh.run[dd] + sh.cnt[wave][dd] + rank[q];
-                    if (dst < begin + m) {  // always, for a consistent segment; never outside it
-                        dk[dst] = k[q];
-                        dv[dst] = v[q];
-                    }
-                }
-            }
-            __syncthreads();
-            sh.run[t] += tot;
-            __syncthreads();
-        }
+        for (uint32_t c0 = 0; c0 < m; c0 += kBigStep)
+            scatter_step(sk, sv, dk, dv, begin + c0, m - c0 < (uint32_t)kBigStep ? m - c0 : (uint32_t)kBigStep, shift,
+                         kRadix - 1, begin, begin + m, sh);
     }
 }
 
@@ -554,10 +576,17 @@ __device__ __forceinline__ void segment_sort_global(uint64_t* __restrict__ keys,
 // depth bits crowd into a few buckets): run A (<= kSegRun) sorted in LDS, run B parked in registers
 // and sorted after it, the two merged by rank; every item's high key half and value gathered by
 // its index in the segment and written in place.  `diff` = the low key bits that vary.
-__device__ __forceinline__ void segment_sort_lsd(uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+// The segment is read from (src_k, src_v) and written to (dst_k, dst_v): the same buffers (in
+// place: every read precedes the first write) or alt -> keys (a piece of a partitioned hot tile).
+// InPlace: dst is ignored and written through pointers based on src (keeps __restrict__ valid).
+template <bool InPlace>
+__device__ __forceinline__ void segment_sort_lsd(const uint64_t* __restrict__ src_k, const uint32_t* __restrict__ src_v,
+                                                 uint64_t* __restrict__ dst_k, uint32_t* __restrict__ dst_v,
                                                  const uint32_t begin, const uint32_t m, const uint32_t diff,
                                                  SegShared& sh)
 {
+    uint64_t* dk = InPlace ? const_cast<uint64_t*>(src_k) : dst_k;
+    uint32_t* dv = InPlace ? const_cast<uint32_t*>(src_v) : dst_v;
     const int t = threadIdx.x;
     const uint32_t na = m < (uint32_t)kSegRun ? m : (uint32_t)kSegRun, nb = m - na;
     uint32_t bk[kRunItems];
@@ -565,10 +594,10 @@ __device__ __forceinline__ void segment_sort_lsd(uint64_t* __restrict__ keys, ui
     for (int q = 0; q < kRunItems; q++) {
         const uint32_t i = t + q * kBlock;
         if (i < na) {
-            sh.k[0][i] = (uint32_t)keys[begin + i];
+            sh.k[0][i] = (uint32_t)src_k[begin + i];
             sh.i[0][i] = i;
         }
-        bk[q] = i < nb ? (uint32_t)keys[begin + kSegRun + i] : 0u;
+        bk[q] = i < nb ? (uint32_t)src_k[begin + kSegRun + i] : 0u;
     }
     __syncthreads();
     const int ca = lds_radix_sort(sh, na, diff);
@@ -626,21 +655,21 @@ __device__ __forceinline__ void segment_sort_lsd(uint64_t* __restrict__ keys, ui
         }
     }
     // gather each item's high key half and value by its index in the segment (the segment is
-    // unmodified until every workgroup thread has gathered), then write in place
+    // unmodified until every workgroup thread has gathered), then write
     uint32_t hi[kSegItems], v[kSegItems];
 #pragma unroll
     for (int q = 0; q < kSegItems; q++) {
         if (fok[q]) {
-            hi[q] = (uint32_t)(keys[begin + fi[q]] >> 32);
-            v[q] = vals[begin + fi[q]];
+            hi[q] = (uint32_t)(src_k[begin + fi[q]] >> 32);
+            v[q] = src_v[begin + fi[q]];
         }
     }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kSegItems; q++) {
         if (fok[q]) {
-            keys[begin + fp[q]] = ((uint64_t)hi[q] << 32) | fk[q];
-            vals[begin + fp[q]] = v[q];
+            dk[begin + fp[q]] = ((uint64_t)hi[q] << 32) | fk[q];
+            dv[begin + fp[q]] = v[q];
         }
     }
 }
@@ -673,28 +702,526 @@ struct BucketShared {
 static_assert(sizeof(BucketShared) >= kSegCap * sizeof(uint64_t), "staging of the keys");
 static_assert(sizeof(BucketShared) >= kSegRun * (sizeof(uint64_t) + sizeof(uint32_t)), "staging of a run");
 
+// ---- hot tiles: the partition queue --------------------------------------------------------
+//
+// A segment of more than kSegCap pairs is not sorted by one workgroup (that costs ~10 ns per pair:
+// a 100K-pair tile took 1 ms) but split among many.  It becomes a RECORD, partitioned stably by
+// one digit -- its top <= 8 varying low-key bits -- in three phases of chunk jobs (kChunk pairs):
+//   REDUCE   AND / OR of the chunk's low key halves        -> the digit (last chunk decides)
+//   HIST     the chunk's digit counts                      -> pool; the last chunk scans them into
+//                                                             every chunk's per-digit destinations
+//   SCATTER  the chunk's pairs, ranked stably, to the other buffer (keys <-> alt)
+// and the last SCATTER cuts the result into pieces by digit: runs of small digits merged up to
+// kSegCap pairs become SMALL jobs (the bucket form of segment_sort_kernel, alt -> keys or in place),
+// a digit of more than kSegCap pairs a new record one digit lower.  Each level fixes the top <= 8
+// varying bits, so the chain ends within 4 levels; pieces left in alt are copied back (COPY jobs).
+// Every piece keeps its pairs in input order between equal digits, so the whole is the stable sort.
+//
+// Jobs live in a queue in scratch, zeroed each call: a producer reserves slots (CAS on `reserve`),
+// writes them and publishes each by setting its tag; a consumer workgroup claims the next index
+// (`head`) and waits until that slot is published or every job is finished (`done` == `reserve`:
+// nothing in flight, so nothing more can come).  Every wait is bounded (kMaxPolls) and flags
+// Q_ERROR when exceeded.  Producers run (they reserved while resident) and publish right after
+// writing, so no wait is on a workgroup that is not running.  Ordering across workgroups (and XCD
+// L2s) is by agent-scope release / acquire: job payload and pair data before the tag, phase data
+// before `pending`.
+constexpr int kChunk = 2 * kBigStep;  // 4096 pairs per chunk job
+#ifndef HIDEGS_QUEUE_BLOCKS
+#define HIDEGS_QUEUE_BLOCKS 256  // queue workers (experiments: tools/build_variant.py)
+#endif
+constexpr int kQueueBlocks = HIDEGS_QUEUE_BLOCKS;
+#ifndef HIDEGS_QUEUE_MIN
+#define HIDEGS_QUEUE_MIN 8192  // segments up to this many pairs: the one-workgroup global form
+#endif
+constexpr int kQueueMin = HIDEGS_QUEUE_MIN;
+constexpr uint32_t kMaxPolls = 1u << 22;
+enum : uint32_t { J_EXIT = 0, J_SMALL, J_COPY, J_REDUCE, J_HIST, J_SCATTER, J_GLOBAL };
+enum : int { Q_HEAD, Q_RESERVE, Q_DONE, Q_NREC, Q_POOL, Q_ERROR, Q_COUNTERS = 8 };
+constexpr int kCtlStride = 32;  // one 128-byte line per counter: polls of one do not queue behind another's atomics
+constexpr int Q_WORDS = Q_COUNTERS * kCtlStride;
+static_assert(Q_WORDS <= kBlock, "identify_ranges_kernel zeroes the counters with one workgroup");
+
+struct BigSeg {
+    uint32_t begin, m, src, chunks;  // pairs [begin, begin + m) of keys (src 0) or alt (src 1)
+    uint32_t and_bits, or_bits;      // REDUCE: AND / OR of the low key halves
+    uint32_t shift, bits;            // the digit: key bits [shift, shift + bits)
+    uint32_t pool;                   // (chunks + 2) x 256 u32: per-chunk counts -> destinations,
+                                     // then the digit starts and the digit totals
+    uint32_t pending;                // jobs of the current phase not yet finished
+    uint32_t pad[2];
+};
+
+struct BigQueue {
+    uint32_t* ctl;  // Q_WORDS counters, zeroed before segment_sort_kernel
+    BigSeg* rec;
+    uint4* job;     // (type | src << 8, a, b, tag): tag 1 once published (zeroed each call)
+    uint32_t* pool;
+    uint32_t rec_cap, job_cap, pool_cap;
+    uint64_t* alt_k;  // the sort's alternate buffers (the global form of a mildly hot tile)
+    uint32_t* alt_v;
+};
+
+#ifdef HIDEGS_QUEUE_TRACE  // experiments only: per-job timestamps (tools/queue_trace.py)
+__device__ unsigned long long g_qtrace[8192][4];  // (type | block << 8 | index << 32, claimed, started, ended)
+__device__ unsigned int g_qtrace_n;
+#endif
+__device__ __forceinline__ uint32_t q_add(uint32_t* p, uint32_t v)
+{
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t q_load(uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
+// polling reads: coherent but without the acquire's cache invalidation (taken once, after the wait)
+__device__ __forceinline__ uint32_t q_peek(uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void fence_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+__device__ __forceinline__ void fence_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); }
+// Cache maintenance is per CU (L1) and per XCD (L2), not per wave, and it is costly (an L2
+// writeback or invalidate per fence; with fences in every wave of every job the chain of a 500K-pair
+// tile ran 1.2 ms): each wave only waits for its own stores to be acknowledged, then after a barrier
+// ONE thread's agent-scope release (L2 writeback) or acquire (invalidate) acts for the workgroup.
+__device__ __forceinline__ void wave_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void q_flag(const BigQueue& q, uint32_t bit)
+{
+    __hip_atomic_fetch_or(&q.ctl[kCtlStride * Q_ERROR], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Jobs a workgroup is about to enqueue, as runs: `count` jobs of one kind.
+constexpr int kMaxRuns = kRadix + 1;
+struct EmitShared {
+    uint4 run[kMaxRuns];  // (type | src << 8, a, b, count)
+    uint32_t off[kMaxRuns + 1];
+    uint32_t nruns, base;
+};
+
+__device__ __forceinline__ void runs_begin(EmitShared& e)
+{
+    e.nruns = 0;
+    e.off[0] = 0;
+}
+
+__device__ __forceinline__ void add_run(EmitShared& e, uint32_t type, uint32_t src, uint32_t a, uint32_t b,
+                                        uint32_t count)
+{
+    if (count == 0) return;
+    e.run[e.nruns] = make_uint4(type | (src << 8), a, b, count);
+    e.off[e.nruns + 1] = e.off[e.nruns] + count;
+    e.nruns++;
+}
+
+// Job j of a run: chunk j of a record, the j-th kChunk piece of a COPY range, or the one job.
+__device__ __forceinline__ uint4 run_job(const uint4 r, const uint32_t j)
+{
+    const uint32_t type = r.x & 0xffu;
+    if (type == J_COPY) {
+        const uint32_t s = j * kChunk;
+        return make_uint4(r.x, r.y + s, r.z - s < (uint32_t)kChunk ? r.z - s : (uint32_t)kChunk, 0u);
+    }
+    if (type == J_REDUCE || type == J_HIST || type == J_SCATTER) return make_uint4(r.x, r.y, j, 0u);
+    return make_uint4(r.x, r.y, r.z, 0u);
+}
+
+// The digit of a record whose varying low-key bits are `diff`: its top <= 8 of them.
+__device__ __forceinline__ void set_digit(BigSeg& s, uint32_t diff)
+{
+    const int top = 31 - __builtin_clz(diff);
+    const int bits = top + 1 < kRadixBits ? top + 1 : kRadixBits;
+    s.shift = (uint32_t)(top + 1 - bits);
+    s.bits = (uint32_t)bits;
+}
+
+// A new record over [begin, begin + m) of buffer src, as the run of jobs that starts it: REDUCE
+// chunk jobs, or -- when the varying bits are known already (`diff` from the parent's SCATTER;
+// ~0u: unknown) -- HIST chunk jobs right away, or a COPY / nothing for a piece with no varying
+// bit.  With the record table or the pool full: one GLOBAL job (the one-workgroup sort).
+// The pool holds (chunks + 4) x 256 u32: per-chunk counts -> destinations, then the digit starts,
+// totals, and AND / OR of each digit's low key halves (the next level's `diff`).
+__device__ __forceinline__ uint4 record_run(const BigQueue& q, uint32_t begin, uint32_t m, uint32_t src,
+                                            uint32_t diff)
+{
+    const uint32_t chunks = (m + kChunk - 1) / kChunk;
+    if (diff == 0u) return make_uint4(J_COPY | (src << 8), begin, m, src ? chunks : 0u);  // already in order
+    const uint32_t need = (chunks + 4) * kRadix;
+    const uint32_t r = __hip_atomic_fetch_add(&q.ctl[kCtlStride * Q_NREC], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t p = ~0u;
+    if (r < q.rec_cap) {
+        p = __hip_atomic_fetch_add(&q.ctl[kCtlStride * Q_POOL], need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint64_t)p + need > q.pool_cap) p = ~0u;
+    }
+    if (p == ~0u) return make_uint4(J_GLOBAL | (src << 8), begin, m, 1u);
+    BigSeg& s = q.rec[r];
+    s.begin = begin;
+    s.m = m;
+    s.src = src;
+    s.chunks = chunks;
+    s.and_bits = 0xffffffffu;
+    s.or_bits = 0u;
+    s.shift = 0u;
+    s.bits = 0u;
+    s.pool = p;
+    s.pending = chunks;
+    if (diff == ~0u) return make_uint4(J_REDUCE, r, 0u, chunks);
+    set_digit(s, diff);
+    return make_uint4(J_HIST, r, 0u, chunks);
+}
+
+__device__ __forceinline__ void add_run(EmitShared& e, const uint4 r) { add_run(e, r.x & 0xffu, r.x >> 8, r.y, r.z, r.w); }
+
+// All threads: enqueue the runs thread 0 put in e (its writes precede the first barrier).
+__device__ __forceinline__ void emit_jobs(const BigQueue& q, EmitShared& e)
+{
+    const int t = threadIdx.x;
+    __syncthreads();
+    const uint32_t nr = e.nruns, total = e.off[nr];
+    if (total == 0) return;  // block-uniform
+    if (t == 0) {
+        // fetch-add, not a CAS loop: 80 records of one level reserving at once retried their CAS
+        // for 160 us
+        uint32_t base = __hip_atomic_fetch_add(&q.ctl[kCtlStride * Q_RESERVE], total, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint64_t)base + total > q.job_cap) {  // beyond the capacity bound of sort_scratch: cannot
+            q_flag(q, 1u);                          // happen; count the lost jobs done so the queue ends
+            __hip_atomic_fetch_add(&q.ctl[kCtlStride * Q_DONE], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            base = ~0u;
+        }
+        e.base = base;
+    }
+    __syncthreads();
+    const uint32_t base = e.base;
+    if (base == ~0u) return;
+    for (uint32_t j = t; j < total; j += kBlock) {
+        uint32_t r = 0;
+        while (e.off[r + 1] <= j) r++;
+        q.job[base + j] = run_job(e.run[r], j - e.off[r]);  // tag (.w) 0: not yet published
+    }
+    wave_stores_done();  // the jobs (and record / pool / pair stores) before the publish below
+    __syncthreads();
+    if (t == 0) fence_release();  // one L2 writeback for the workgroup (see wave_stores_done)
+    __syncthreads();
+    // publish: each slot's tag becomes 1 (slots publish independently -- a global publication
+    // order would chain every producer behind the one that reserved before it: 80 records of one
+    // level published one after another took 300 us)
+    for (uint32_t j = t; j < total; j += kBlock)
+        __hip_atomic_store(&q.job[base + j].w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Thread t's result: the number of the cnt <= kChunk keys at sk[base..] whose digit is t.
+__device__ __forceinline__ uint32_t chunk_hist(const uint64_t* sk, const uint32_t base, const uint32_t cnt,
+                                               const int shift, const uint32_t mask, BigShared& sh)
+{
+    const int t = threadIdx.x;
+    sh.hist[t] = 0u;
+    __syncthreads();
+    uint32_t dg[kChunk / kBlock];
+#pragma unroll
+    for (int u = 0; u < kChunk / kBlock; u++) {
+        const uint32_t i = t + u * kBlock;
+        dg[u] = i < cnt ? digit_of(sk[base + i], shift, mask) : ~0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kChunk / kBlock; u++)
+        if (dg[u] != ~0u) atomicAdd(&sh.hist[dg[u]], 1u);
+    __syncthreads();
+    return sh.hist[t];
+}
+
+// After every chunk's counts are in the record's pool (col = this thread's digit column): every
+// chunk's destination of each digit (begin + digit start + the digit's count in the chunks before
+// it), the digit starts and totals, and the AND / OR rows the SCATTER jobs gather into.
+__device__ __forceinline__ void plan_scatter(uint32_t* col, const uint32_t chunks, const uint32_t begin, BigShared& sh)
+{
+    constexpr uint32_t U = 8;  // independent loads in flight: the column is in other XCDs' writes
+    uint32_t tot = 0u;
+    for (uint32_t j0 = 0; j0 < chunks; j0 += U) {
+        uint32_t x[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) x[u] = j0 + u < chunks ? col[(j0 + u) * kRadix] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) tot += x[u];
+    }
+    uint32_t dummy;
+    const uint32_t start = block_exclusive_scan(tot, sh.wave, &dummy);
+    uint32_t run = begin + start;
+    for (uint32_t j0 = 0; j0 < chunks; j0 += U) {
+        uint32_t x[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) x[u] = j0 + u < chunks ? col[(j0 + u) * kRadix] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            if (j0 + u < chunks) col[(j0 + u) * kRadix] = run;
+            run += x[u];
+        }
+    }
+    col[chunks * kRadix] = start;
+    col[(chunks + 1) * kRadix] = tot;
+    col[(chunks + 2) * kRadix] = 0xffffffffu;
+    col[(chunks + 3) * kRadix] = 0u;
+}
+
 union SegLds {
     SegShared lsd;
     BucketShared bucket;
     BigShared big;
+    struct {
+        BigShared big;
+        EmitShared emit;
+    } queue;
 };
 
-// Workgroup b sorts segment b in place by the low 32 key bits: the bucket form, its LSD fallback
-// for crowded buckets, or (more than kSegCap pairs) the global form through alt_k / alt_v.
+// One segment of m <= kSegCap pairs sorted by the low 32 key bits: the bucket form, or its LSD
+// fallback for crowded buckets (segment_sort_kernel carries the same code inline).  InPlace: (src_k, src_v) == (dst_k, dst_v); otherwise the pairs
+// are read from alt and written to keys (a piece of a partitioned hot tile).
+template <bool InPlace>
+__device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k, const uint32_t* __restrict__ src_v,
+                                             uint64_t* __restrict__ dst_k, uint32_t* __restrict__ dst_v,
+                                             const uint32_t begin, const uint32_t m, SegLds& lds, uint32_t* s_and,
+                                             uint32_t* s_or, uint32_t* s_max)
+{
+    uint64_t* dk = InPlace ? const_cast<uint64_t*>(src_k) : dst_k;
+    uint32_t* dv = InPlace ? const_cast<uint32_t*>(src_v) : dst_v;
+    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
+    uint64_t k[kSegItems];
+    uint32_t v[kSegItems];
+    uint32_t a = 0xffffffffu, o = 0;
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            k[q] = src_k[begin + i];
+            v[q] = src_v[begin + i];
+            a &= (uint32_t)k[q];
+            o |= (uint32_t)k[q];
+        }
+    }
+    BucketShared& sh = lds.bucket;
+    for (int i = t; i < kBuckets; i += kBlock) sh.fill[i] = 0u;
+    wave_and_or(a, o);
+    if (lane == 0) {
+        s_and[wave] = a;
+        s_or[wave] = o;
+    }
+    __syncthreads();
+    uint32_t diff;
+    {
+        uint32_t aa = 0xffffffffu, oo = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; w++) {
+            aa &= s_and[w];
+            oo |= s_or[w];
+        }
+        diff = aa ^ oo;  // low key bits that vary over the segment
+    }
+    if (diff == 0) {  // equal low keys: the input order is the stable order
+        if (!InPlace) {
+#pragma unroll
+            for (int q = 0; q < kSegItems; q++) {
+                const uint32_t i = t + q * kBlock;
+                if (i < m) {
+                    dk[begin + i] = k[q];
+                    dv[begin + i] = v[q];
+                }
+            }
+        }
+        return;
+    }
+    const int top = 31 - __builtin_clz(diff);
+    const int dbits = top + 1 < kBucketBits ? top + 1 : kBucketBits;
+    const int shift = top + 1 - dbits;
+    const uint32_t dmask = (1u << dbits) - 1u;
+    const uint32_t lowmask = (uint32_t)((1ull << shift) - 1ull);
+
+    // 1. bucket histogram
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++)
+        if (t + q * kBlock < m) atomicAdd(&sh.fill[((uint32_t)k[q] >> shift) & dmask], 1u);
+    __syncthreads();
+    // 2. bucket starts (exclusive scan, 4 buckets per thread) and the fullest bucket
+    uint32_t c[kBuckets / kBlock], sum = 0, mx = 0;
+#pragma unroll
+    for (int j = 0; j < kBuckets / kBlock; j++) {
+        c[j] = sh.fill[t * (kBuckets / kBlock) + j];
+        sum += c[j];
+        mx = c[j] > mx ? c[j] : mx;
+    }
+    uint32_t dummy;
+    uint32_t pre = block_exclusive_scan(sum, s_max, &dummy);  // its barriers order the reads above
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint32_t y = __shfl_xor(mx, s, kWave);
+        mx = y > mx ? y : mx;
+    }
+    if (lane == 0) s_and[wave] = mx;
+#pragma unroll
+    for (int j = 0; j < kBuckets / kBlock; j++) {
+        sh.start[t * (kBuckets / kBlock) + j] = pre;
+        sh.fill[t * (kBuckets / kBlock) + j] = pre;
+        pre += c[j];
+    }
+    __syncthreads();
+    uint32_t fullest = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; w++) fullest = s_and[w] > fullest ? s_and[w] : fullest;
+    if (fullest > (uint32_t)kMaxBucket || shift + kIndexBits > 32) {  // crowded depths, or fields too
+        // wide for 32 bits: the LSD form (block-uniform branch)
+        __syncthreads();
+        segment_sort_lsd<InPlace>(src_k, src_v, dst_k, dst_v, begin, m, diff, lds.lsd);
+        return;
+    }
+    // 3. fill the buckets in any order
+    uint32_t me[kSegItems];
+    uint32_t bucket[kSegItems];
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            bucket[q] = ((uint32_t)k[q] >> shift) & dmask;
+            me[q] = (((uint32_t)k[q] & lowmask) << kIndexBits) | i;
+            sh.comb[atomicAdd(&sh.fill[bucket[q]], 1u)] = me[q];
+        }
+    }
+    __syncthreads();
+    // 4. exact rank inside the bucket
+    uint32_t pos[kSegItems];
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        if (t + q * kBlock < m) {
+            const uint32_t s0 = sh.start[bucket[q]], e0 = sh.fill[bucket[q]];
+            uint32_t rank = 0;
+            for (uint32_t j = s0; j < e0; j++) rank += sh.comb[j] < me[q] ? 1u : 0u;
+            pos[q] = s0 + rank;
+        }
+    }
+    // 5. stage (key, value) by final position in LDS, then store the segment contiguously (stores
+    //    straight from registers scatter 8- and 4-byte writes over the segment: 78 -> 50 us at 8M pairs)
+    __syncthreads();
+    uint64_t* stage_k = reinterpret_cast<uint64_t*>(&sh);
+    uint32_t* stage_v = reinterpret_cast<uint32_t*>(stage_k + kSegRun);
+    const bool together = m <= (uint32_t)kSegRun;  // block-uniform
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        if (t + q * kBlock < m) {
+            stage_k[pos[q]] = k[q];
+            if (together) stage_v[pos[q]] = v[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) {
+            dk[begin + i] = stage_k[i];
+            if (together) dv[begin + i] = stage_v[i];
+        }
+    }
+    if (together) return;
+    __syncthreads();
+    stage_v = reinterpret_cast<uint32_t*>(&sh);
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++)
+        if (t + q * kBlock < m) stage_v[pos[q]] = v[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kSegItems; q++) {
+        const uint32_t i = t + q * kBlock;
+        if (i < m) dv[begin + i] = stage_v[i];
+    }
+}
+
+// A record's first two phases (REDUCE, HIST) run by the workgroup that opens it, inside
+// segment_sort_kernel where the other segments' sorts hide them, for a tile of up to kOpenLocal
+// pairs: the queue then starts at the SCATTER jobs.
+#ifndef HIDEGS_OPEN_LOCAL
+#define HIDEGS_OPEN_LOCAL 24576
+#endif
+constexpr int kOpenLocal = HIDEGS_OPEN_LOCAL;
+__device__ __forceinline__ void open_local(const uint64_t* keys, const BigQueue& q, const uint32_t begin,
+                                           const uint32_t m, BigShared& sh, EmitShared& e, uint32_t* s_and,
+                                           uint32_t* s_or)
+{
+    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
+    uint32_t a = 0xffffffffu, o = 0u;
+    for (uint32_t i0 = 0; i0 < m; i0 += kChunk) {
+        uint32_t x[kChunk / kBlock];
+#pragma unroll
+        for (int u = 0; u < kChunk / kBlock; u++) {
+            const uint32_t i = i0 + u * kBlock + t;
+            x[u] = (uint32_t)keys[begin + (i < m ? i : 0u)];  // a repeat changes no AND / OR
+        }
+#pragma unroll
+        for (int u = 0; u < kChunk / kBlock; u++) {
+            a &= x[u];
+            o |= x[u];
+        }
+    }
+    wave_and_or(a, o);
+    if (lane == 0) {
+        s_and[wave] = a;
+        s_or[wave] = o;
+    }
+    __syncthreads();
+    for (int w = 0; w < kWavesPerBlock; w++) {
+        a &= s_and[w];
+        o |= s_or[w];
+    }
+    const uint32_t diff = a ^ o;
+    if (diff == 0u) return;  // equal low keys: in stable order already (block-uniform)
+    if (t == 0) {
+        runs_begin(e);
+        const uint4 r = record_run(q, begin, m, 0u, diff);
+        e.run[0] = r;
+        e.base = (r.x & 0xffu) == J_HIST ? q.rec[r.y].pool : ~0u;
+        if (e.base == ~0u) add_run(e, r);  // the table or pool is full: a GLOBAL job
+    }
+    __syncthreads();
+    const uint32_t pool = e.base, rec = e.run[0].y, chunks = (m + kChunk - 1) / kChunk;
+    if (pool != ~0u) {
+        const int top = 31 - __builtin_clz(diff);  // the record's digit (set_digit)
+        const int bits = top + 1 < kRadixBits ? top + 1 : kRadixBits;
+        const int shift = top + 1 - bits;
+        const uint32_t mask = (1u << bits) - 1u;
+        uint32_t* col = q.pool + pool + t;
+        for (uint32_t c = 0; c < chunks; c++) {
+            const uint32_t c0 = c * kChunk;
+            col[c * kRadix] = chunk_hist(keys, begin + c0, m - c0 < (uint32_t)kChunk ? m - c0 : (uint32_t)kChunk,
+                                         shift, mask, sh);
+        }
+        __syncthreads();
+        plan_scatter(col, chunks, begin, sh);
+        if (t == 0) {
+            runs_begin(e);
+            add_run(e, J_SCATTER, 0u, rec, 0u, chunks);  // pending == chunks already
+        }
+    }
+    emit_jobs(q, e);
+}
+
+// Workgroup b sorts segment b in place by the low 32 key bits (sort_segment); a segment of more
+// than kSegCap pairs becomes a record of the partition queue (big_segment_kernel runs it).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_SEG_WAVES))) void segment_sort_kernel(
-    uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint2* __restrict__ ranges,
-    uint64_t* __restrict__ alt_k, uint32_t* __restrict__ alt_v)
+    uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint2* __restrict__ ranges, const BigQueue q)
 {
     __shared__ __attribute__((aligned(16))) SegLds lds;
     __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock], s_max[kWavesPerBlock];
-    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
     const uint2 r = ranges[blockIdx.x];
     const uint32_t begin = r.x, m = r.y - r.x;
     if (r.y <= r.x + 1) return;  // absent or single pair: already in place
     if (m > (uint32_t)kSegCap) {
-        segment_sort_global(keys, vals, alt_k, alt_v, begin, m, lds.big);
+        if (m <= (uint32_t)kQueueMin) {  // mildly hot: this workgroup, overlapped with the others
+            segment_sort_global(keys, vals, q.alt_k, q.alt_v, begin, m, lds.big);
+            return;
+        }
+        if (m <= (uint32_t)kOpenLocal) {
+            open_local(keys, q, begin, m, lds.queue.big, lds.queue.emit, s_and, s_or);
+            return;
+        }
+        if (threadIdx.x == 0) {
+            runs_begin(lds.queue.emit);
+            add_run(lds.queue.emit, record_run(q, begin, m, 0u, ~0u));
+        }
+        emit_jobs(q, lds.queue.emit);
         return;
     }
+    // sort_segment<true>'s code, written out: as an inlined call the same code spills 16 VGPRs at
+    // the 72-VGPR budget of HIDEGS_SEG_WAVES (the register allocator sees it differently)
+    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
     uint64_t k[kSegItems];
     uint32_t v[kSegItems];
     uint32_t a = 0xffffffffu, o = 0;
@@ -767,7 +1294,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
     if (fullest > (uint32_t)kMaxBucket || shift + kIndexBits > 32) {  // crowded depths, or fields too
         // wide for 32 bits: the LSD form (block-uniform branch)
         __syncthreads();
-        segment_sort_lsd(keys, vals, begin, m, diff, lds.lsd);
+        segment_sort_lsd<true>(keys, vals, nullptr, nullptr, begin, m, diff, lds.lsd);
         return;
     }
     // 3. fill the buckets in any order
@@ -830,6 +1357,255 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
     }
 }
 
+
+// The last workgroup to finish a phase job of record s goes on (returns true); the others return
+// false.  The caller's global writes are published before the count-down.
+__device__ __forceinline__ bool finish_phase(BigSeg& s, uint32_t* s_flag)
+{
+    wave_stores_done();
+    __syncthreads();
+    if (threadIdx.x == 0) *s_flag = q_add(&s.pending, 0xffffffffu) == 1u;  // release + acquire
+    __syncthreads();
+    return *s_flag != 0;
+}
+
+// The partition queue's workers: kQueueBlocks workgroups take jobs until none is left or in
+// flight.  With no hot tile (the common case) every workgroup reads one counter and exits.
+__global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                             uint64_t* __restrict__ alt_k,
+                                                             uint32_t* __restrict__ alt_v, const BigQueue q)
+{
+    __shared__ __attribute__((aligned(16))) SegLds lds;
+    __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock], s_max[kWavesPerBlock];
+    __shared__ uint4 s_job;
+    __shared__ uint32_t s_flag;
+    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
+    BigShared& sh = lds.queue.big;
+    EmitShared& e = lds.queue.emit;
+    if (t == 0) s_flag = q_peek(&q.ctl[kCtlStride * Q_RESERVE]);
+    __syncthreads();
+    if (s_flag == 0) return;  // nothing was queued (the queue was filled by the previous launch)
+#ifdef HIDEGS_QUEUE_TRACE
+    unsigned long long t_claim = 0, t_got = 0;
+    uint32_t t_index = 0;
+#endif
+    for (;;) {
+        __syncthreads();  // the previous job's LDS use is over
+        if (t == 0) {
+            const uint32_t i = q_add(&q.ctl[kCtlStride * Q_HEAD], 1u);
+#ifdef HIDEGS_QUEUE_TRACE
+            t_claim = wall_clock64();
+            t_index = i;
+#endif
+            uint4 job = make_uint4(J_EXIT, 0u, 0u, 0u);
+            uint32_t polls = 0, backoff = 1;
+            for (; polls < kMaxPolls; polls++) {
+                if (i < q.job_cap && q_peek(&q.job[i].w) != 0u) {
+                    fence_acquire();  // for the whole workgroup (see wave_stores_done)
+                    job = q.job[i];
+                    break;
+                }
+                if (q_peek(&q.ctl[kCtlStride * Q_DONE]) == q_peek(&q.ctl[kCtlStride * Q_RESERVE])) {
+                    // confirm in order: `done` (acquire) before `reserve`
+                    const uint32_t d = q_load(&q.ctl[kCtlStride * Q_DONE]);
+                    const uint32_t r = q_load(&q.ctl[kCtlStride * Q_RESERVE]);
+                    if (d == r && i >= r) break;  // nothing queued, nothing in flight: the end
+                }
+                for (uint32_t k = 0; k < backoff; k++) __builtin_amdgcn_s_sleep(8);  // ~0.2 us each
+                backoff = backoff < 16u ? 2u * backoff : 16u;
+            }
+            if (polls == kMaxPolls) q_flag(q, 4u);
+            s_job = job;
+#ifdef HIDEGS_QUEUE_TRACE
+            t_got = wall_clock64();
+#endif
+        }
+        __syncthreads();
+        const uint4 job = s_job;
+        const uint32_t type = job.x & 0xffu, src = job.x >> 8;
+        if (type == J_EXIT) return;
+
+        if (type == J_SMALL) {
+            if (src)
+                sort_segment<false>(alt_k, alt_v, keys, vals, job.y, job.z, lds, s_and, s_or, s_max);
+            else
+                sort_segment<true>(keys, vals, nullptr, nullptr, job.y, job.z, lds, s_and, s_or, s_max);
+        } else if (type == J_COPY) {
+            for (uint32_t i = t; i < job.z; i += kBlock) {
+                keys[job.y + i] = alt_k[job.y + i];
+                vals[job.y + i] = alt_v[job.y + i];
+            }
+        } else if (type == J_GLOBAL) {
+            if (src) {
+                for (uint32_t i = t; i < job.z; i += kBlock) {
+                    keys[job.y + i] = alt_k[job.y + i];
+                    vals[job.y + i] = alt_v[job.y + i];
+                }
+                __syncthreads();
+            }
+            segment_sort_global(keys, vals, alt_k, alt_v, job.y, job.z, sh);
+        } else {  // a chunk job of record job.y
+            BigSeg& s = q.rec[job.y];
+            const uint32_t c = job.z, begin = s.begin, m = s.m, chunks = s.chunks;
+            const uint32_t c0 = c * kChunk, cnt = m - c0 < (uint32_t)kChunk ? m - c0 : (uint32_t)kChunk;
+            const uint64_t* sk = s.src ? alt_k : keys;
+            uint32_t* col = q.pool + s.pool + t;  // this thread's digit column
+            if (type == J_REDUCE) {
+                uint32_t a = 0xffffffffu, o = 0u;
+#pragma unroll
+                for (int u = 0; u < kChunk / kBlock; u++) {
+                    const uint32_t i = t + u * kBlock;
+                    if (i < cnt) {
+                        const uint32_t x = (uint32_t)sk[begin + c0 + i];
+                        a &= x;
+                        o |= x;
+                    }
+                }
+                wave_and_or(a, o);
+                if (lane == 0) {
+                    s_and[wave] = a;
+                    s_or[wave] = o;
+                }
+                __syncthreads();
+                if (t == 0) {
+                    for (int w = 0; w < kWavesPerBlock; w++) {
+                        a &= s_and[w];
+                        o |= s_or[w];
+                    }
+                    __hip_atomic_fetch_and(&s.and_bits, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_or(&s.or_bits, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (finish_phase(s, &s_flag)) {
+                    if (t == 0) {
+                        runs_begin(e);
+                        const uint32_t diff = q_load(&s.and_bits) ^ q_load(&s.or_bits);
+                        if (diff == 0) {  // equal low keys: already in stable order
+                            if (s.src) add_run(e, J_COPY, 1u, begin, m, chunks);
+                        } else {
+                            set_digit(s, diff);
+                            s.pending = chunks;
+                            add_run(e, J_HIST, 0u, job.y, 0u, chunks);
+                        }
+                    }
+                    emit_jobs(q, e);
+                }
+            } else if (type == J_HIST) {
+                const int shift = (int)s.shift;
+                const uint32_t mask = (1u << s.bits) - 1u;
+                col[c * kRadix] = chunk_hist(sk, begin + c0, cnt, shift, mask, sh);
+                if (finish_phase(s, &s_flag)) {
+                    plan_scatter(col, chunks, begin, sh);
+                    if (t == 0) {
+                        s.pending = chunks;
+                        runs_begin(e);
+                        add_run(e, J_SCATTER, 0u, job.y, 0u, chunks);
+                    }
+                    emit_jobs(q, e);
+                }
+            } else {  // J_SCATTER
+                const int shift = (int)s.shift;
+                const uint32_t mask = (1u << s.bits) - 1u;
+                const uint32_t dst = s.src ^ 1u;
+                const uint32_t* sv = s.src ? alt_v : vals;
+                uint64_t* dk = dst ? alt_k : keys;
+                uint32_t* dv = dst ? alt_v : vals;
+                sh.run[t] = col[c * kRadix];
+                sh.aux[0][t] = 0xffffffffu;
+                sh.aux[1][t] = 0u;
+                for (uint32_t b0 = 0; b0 < cnt; b0 += kBigStep)
+                    scatter_step<true>(sk, sv, dk, dv, begin + c0 + b0,
+                                       cnt - b0 < (uint32_t)kBigStep ? cnt - b0 : (uint32_t)kBigStep, shift, mask,
+                                       begin, begin + m, sh);
+                // this chunk's per-digit AND / OR into the record's (digits it holds only)
+                if (sh.aux[0][t] != 0xffffffffu || sh.aux[1][t] != 0u) {
+                    __hip_atomic_fetch_and(&col[(chunks + 2) * kRadix], sh.aux[0][t], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_or(&col[(chunks + 3) * kRadix], sh.aux[1][t], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (finish_phase(s, &s_flag)) {
+                    // cut the record into pieces, one thread per digit:
+                    //  * a digit of more than kSegCap pairs: a record of the next level (its varying
+                    //    bits are known: HIST jobs directly);
+                    //  * a digit of more than kSegRun pairs: a SMALL piece of its own;
+                    //  * other non-empty digits: SMALL pieces of consecutive digits whose starts share
+                    //    a kSegRun-aligned window (so a piece holds < 2 * kSegRun = kSegCap pairs).
+                    const uint32_t n_d = col[(chunks + 1) * kRadix];  // 0 above the digit mask
+                    const uint32_t s_d = col[chunks * kRadix];        // relative start
+                    const uint32_t diff_d = col[(chunks + 2) * kRadix] ^ col[(chunks + 3) * kRadix];
+                    if (shift == 0) {  // every varying bit is placed: the record is sorted
+                        if (t == 0) {
+                            runs_begin(e);
+                            if (dst) add_run(e, J_COPY, 1u, begin, m, chunks);
+                        }
+                    } else {
+                        const bool nonempty = n_d != 0u, solo = n_d > (uint32_t)kSegRun;
+                        uint32_t* pv = sh.hist;  // previous non-empty digit + 1: inclusive max-scan
+                        uint32_t* nx = sh.run;   // start of the next piece: suffix min-scan
+                        pv[t] = nonempty ? (uint32_t)t + 1u : 0u;
+                        sh.cnt[0][t] = solo;
+                        sh.cnt[1][t] = s_d;
+                        __syncthreads();
+                        for (int o = 1; o < kRadix; o <<= 1) {
+                            const uint32_t x = t >= o ? pv[t - o] : 0u;
+                            __syncthreads();
+                            pv[t] = x > pv[t] ? x : pv[t];
+                            __syncthreads();
+                        }
+                        const uint32_t prev = t ? pv[t - 1] : 0u;
+                        const bool boundary = nonempty && (prev == 0u || solo || sh.cnt[0][prev - 1] != 0u ||
+                                                           (s_d / kSegRun) != (sh.cnt[1][prev - 1] / kSegRun));
+                        nx[t] = boundary ? s_d : m;
+                        __syncthreads();
+                        for (int o = 1; o < kRadix; o <<= 1) {
+                            const uint32_t x = t + o < kRadix ? nx[t + o] : m;
+                            __syncthreads();
+                            nx[t] = x < nx[t] ? x : nx[t];
+                            __syncthreads();
+                        }
+                        const uint32_t next = t + 1 < kRadix ? nx[t + 1] : m;
+                        uint4 run = make_uint4(0u, 0u, 0u, 0u);
+                        if (boundary) {
+                            if (n_d > (uint32_t)kSegCap)
+                                run = record_run(q, begin + s_d, n_d, dst, diff_d);
+                            else if (next - s_d > 1u || dst)
+                                run = make_uint4(J_SMALL | (dst << 8), begin + s_d, next - s_d, 1u);
+                        }
+                        uint32_t nruns, total;
+                        const uint32_t ri = block_exclusive_scan(run.w ? 1u : 0u, sh.wave, &nruns);
+                        const uint32_t ro = block_exclusive_scan(run.w, sh.wave, &total);
+                        if (run.w) {
+                            e.run[ri] = run;
+                            e.off[ri] = ro;
+                        }
+                        if (t == 0) {
+                            e.nruns = nruns;
+                            e.off[nruns] = total;
+                        }
+                    }
+                    emit_jobs(q, e);
+                }
+            }
+        }
+        // `done` only ends the queue (no data hangs on it): the jobs this one queued are
+        // published already, and the pairs it wrote are for kernel completion or a publish
+        __syncthreads();
+        if (t == 0) __hip_atomic_fetch_add(&q.ctl[kCtlStride * Q_DONE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef HIDEGS_QUEUE_TRACE
+        if (t == 0) {
+            const unsigned int slot = atomicAdd(&g_qtrace_n, 1u);
+            if (slot < 8192) {
+                const uint32_t last = (type == J_REDUCE || type == J_HIST || type == J_SCATTER) && s_flag ? 0x80u : 0u;
+                g_qtrace[slot][0] = (unsigned long long)(type | last | (blockIdx.x << 8)) | ((unsigned long long)t_index << 32);
+                g_qtrace[slot][1] = t_claim;
+                g_qtrace[slot][2] = t_got;
+                g_qtrace[slot][3] = wall_clock64();
+            }
+        }
+#endif
+    }
+}
+
 // ============================== tile ranges ====================================
 
 // Tile ids >= num_tiles violate the caller contract; their entries are skipped rather
@@ -840,10 +1616,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
 // >= num_tiles are skipped.  Each thread checks 4 consecutive keys (two 16-byte loads) and the
 // key before them; only the rare boundaries write.
 constexpr int kRangeKeys = 4;
+// zero (or NULL): the partition queue, reset for the segment_sort_kernel that follows -- its
+// Q_WORDS counters and its job_cap slots (slot tags read 0 until published).
 __global__ __launch_bounds__(kBlock) void identify_ranges_kernel(const uint64_t* __restrict__ keys, long long n,
                                                                  uint2* __restrict__ ranges, uint32_t num_tiles,
-                                                                 uint32_t tile_mask)
+                                                                 uint32_t tile_mask, const BigQueue zero)
 {
+    if (zero.ctl) {
+        if (blockIdx.x == 0 && threadIdx.x < Q_WORDS) zero.ctl[threadIdx.x] = 0u;
+        for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < zero.job_cap; j += gridDim.x * kBlock)
+            zero.job[j] = make_uint4(0u, 0u, 0u, 0u);
+    }
     const long long i0 = ((long long)blockIdx.x * kBlock + threadIdx.x) * kRangeKeys;
     if (i0 >= n) return;
     uint32_t tile[kRangeKeys];
@@ -891,19 +1674,39 @@ constexpr long long kSegmentedMinAvg = 64;   // pairs per segment on average, el
                                              // workgroup per ~30-pair segment (distCUDA2's 48-bit Morton
                                              // keys of 2M points) costs more than the 4 low-digit passes
 
+// Capacities of the partition queue for n pairs.  Every record holds > kSegCap pairs and the
+// records of one level are disjoint: <= n / 2049 per level, 5 levels (4 digits + the copy).  A
+// record queues <= 3 jobs per chunk of 4096 pairs and <= 2 pieces per kSegRun pairs (a piece lies in
+// one kSegRun window or is a digit of its own) -- under n / 39 jobs in all, so job_cap (n / 24,
+// zeroed every call: n / 1.5 bytes) cannot overflow.  The pool ((chunks + 4) x 256 u32 per record)
+// is sized for a few hot tiles' worth; a record that finds it (or the record table) full is sorted
+// by one workgroup instead (a GLOBAL job) -- slower, same result.
+BigQueue queue_caps(long long n)
+{
+    BigQueue q{};
+    q.rec_cap = (uint32_t)(5 * (n / (kSegCap + 1)) + 8);
+    q.job_cap = (uint32_t)(n / 24 + 1024);
+    q.pool_cap = (uint32_t)(n / 2 + 16 * kRadix);
+    return q;
+}
+
 template <typename K>
 size_t sort_scratch(long long n)
 {
     const int nt = ceil_div(n, kTile);
     size_t b = align_up((size_t)n * sizeof(K)) + align_up((size_t)n * sizeof(uint32_t)) +
                align_up((size_t)kRadix * nt * sizeof(uint32_t)) + align_up(kRadix * sizeof(uint32_t));
-    if (sizeof(K) == 8)  // segmented path: the segment ranges
-        b += align_up(sizeof(uint2) << kMaxSegmentBits);
+    if (sizeof(K) == 8) {  // segmented path: the segment ranges and the partition queue
+        const BigQueue q = queue_caps(n);
+        b += align_up(sizeof(uint2) << kMaxSegmentBits) + align_up(Q_WORDS * sizeof(uint32_t)) +
+             align_up((size_t)q.rec_cap * sizeof(BigSeg)) + align_up((size_t)q.job_cap * sizeof(uint4)) +
+             align_up((size_t)q.pool_cap * sizeof(uint32_t));
+    }
     return b;
 }
 
 __global__ void identify_ranges_kernel(const uint64_t* __restrict__ keys, long long n, uint2* __restrict__ ranges,
-                                       uint32_t num_tiles, uint32_t tile_mask);
+                                       uint32_t num_tiles, uint32_t tile_mask, const BigQueue zero);
 
 // ranges_out (num_tiles entries) set: the tile ranges of the sorted keys are written too, with
 // identify_tile_ranges' semantics; the caller guarantees key >> 32 < num_tiles.
@@ -983,13 +1786,21 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
             nseg = num_tiles;
             tile_mask = 0xffffffffu;
         }
+        BigQueue q = queue_caps(n);
+        q.ctl = c.take<uint32_t>(Q_WORDS);
+        q.rec = c.take<BigSeg>(q.rec_cap);
+        q.job = c.take<uint4>(q.job_cap);
+        q.pool = c.take<uint32_t>(q.pool_cap);
+        q.alt_k = reinterpret_cast<uint64_t*>(alt_k);
+        q.alt_v = alt_v;
         uint64_t* ko = reinterpret_cast<uint64_t*>(keys_out);
         if (hipMemsetAsync(ranges, 0, sizeof(uint2) * nseg, stream) != hipSuccess)
             return fail(HIDEGS_E_HIP, std::string(what) + ": memset failed");
         HIDEGS_LAUNCH("segment_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock * kRangeKeys)), dim3(kBlock), 0, stream,
-                      (const uint64_t*)ko, n, ranges, (uint32_t)nseg, tile_mask);
-        HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out, ranges,
-                      reinterpret_cast<uint64_t*>(alt_k), alt_v);
+                      (const uint64_t*)ko, n, ranges, (uint32_t)nseg, tile_mask, q);
+        HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out, ranges, q);
+        HIDEGS_LAUNCH("big_segments", big_segment_kernel, dim3(kQueueBlocks), dim3(kBlock), 0, stream, ko, vals_out,
+                      reinterpret_cast<uint64_t*>(alt_k), alt_v, q);
     } else if (ranges_out) {
         if (int rc = check_launch(what, stream, 0)) return rc;
         return identify_tile_ranges(reinterpret_cast<const uint64_t*>(keys_out), n,
@@ -1053,7 +1864,7 @@ int identify_tile_ranges(const uint64_t* keys, long long n, uint32_t* ranges, in
     if (n == 0) return check_launch("identify_tile_ranges", stream, 0);
     if (!keys) return fail(HIDEGS_E_ARG, "identify_tile_ranges: NULL keys");
     HIDEGS_LAUNCH("identify_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock * kRangeKeys)), dim3(kBlock), 0, stream, keys, n,
-                       reinterpret_cast<uint2*>(ranges), (uint32_t)num_tiles, 0xffffffffu);
+                       reinterpret_cast<uint2*>(ranges), (uint32_t)num_tiles, 0xffffffffu, BigQueue{});
     return check_launch("identify_tile_ranges", stream, 0);
 }
 
@@ -1109,4 +1920,19 @@ uint32_t hidegs_higher_msb(uint32_t n)
     return bits;
 }
 
+#ifdef HIDEGS_QUEUE_TRACE
+// experiments only: copy out (and reset) the partition queue's job trace; returns the job count
+int hidegs_debug_queue_trace(unsigned long long* host, int max_jobs)
+{
+    unsigned int n = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(&n, HIP_SYMBOL(hidegs::g_qtrace_n), sizeof(n)) != hipSuccess)
+        return -1;
+    const int m = (int)(n < (unsigned)max_jobs ? n : (unsigned)max_jobs);
+    if (m > 0 && hipMemcpyFromSymbol(host, HIP_SYMBOL(hidegs::g_qtrace), (size_t)m * 4 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    n = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hidegs::g_qtrace_n), &n, sizeof(n)) != hipSuccess) return -1;
+    return m;
+}
+#endif
 }  // extern "C"

@@ -236,3 +236,72 @@ def test_config5_scale_4k_frame_sort_tile_pairs():
     assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
     assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
     assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, 32400))
+
+
+def _hot_tile_case(case, g):
+    """Low key halves of one hot tile (csrc/primitives.hip's partition queue) by case."""
+    if case == "uniform":
+        n = 100_000
+        return g.uniform(0.2, 100.0, n).astype(np.float32).view(np.uint32).astype(np.uint64)
+    if case == "dups":  # 5 depths: the first digit leaves pieces of ~12K equal keys (copied back)
+        return g.choice(np.array([3.5, 7.0, 7.25, 40.0, 99.0], np.float32), 60_000).view(np.uint32).astype(np.uint64)
+    if case == "equal":  # nothing varies: the record ends after its first phase
+        return np.full(30_000, np.float32(12.5).view(np.uint32), np.uint64)
+    if case == "full32":  # bit 31 set on half of them, 8 varying bits per level
+        return g.integers(0, 2**32, 200_000, dtype=np.uint64)
+    if case == "skewed":  # 90% share each byte above the lowest: a chain of 4 records deep
+        n = 400_000
+        parts = [np.where(g.random(n) < 0.9, 0, g.integers(0, 256, n)).astype(np.uint64) for _ in range(3)]
+        low = g.integers(0, 256, n).astype(np.uint64)
+        return (parts[0] << np.uint64(24)) | (parts[1] << np.uint64(16)) | (parts[2] << np.uint64(8)) | low
+    if case == "pieces":  # digit runs just under / over the piece size: merged runs and 2049-pair records
+        reps = np.array([2047, 2048, 2049, 1, 1500, 600, 4097, 2], np.int64)
+        vals = np.arange(reps.size, dtype=np.uint64) << np.uint64(24)
+        low = np.repeat(vals, reps) | g.integers(0, 1 << 16, int(reps.sum())).astype(np.uint64)
+        return low
+    raise ValueError(case)
+
+
+@pytest.mark.parametrize("case", ["uniform", "dups", "equal", "full32", "skewed", "pieces"])
+def test_hot_tile_partition_queue_bit_exact(case):
+    """A tile far over the 2048-pair capacity of one workgroup's sort goes through the partition
+    queue (REDUCE / HIST / SCATTER chunk jobs, then pieces): uniform depths, few distinct depths,
+    all equal, full 32-bit low halves, a skew that chains records 4 levels deep, and digit runs at
+    the piece-size boundaries -- among 500K ordinary pairs, bit-identical to the oracle's stable
+    sort, through sort_pairs and sort_tile_pairs."""
+    g = np.random.default_rng(sum(map(ord, case)))
+    T = 1024
+    keys, vals = raster_like_keys(500_000, T, 77)
+    low = _hot_tile_case(case, g)
+    hot = np.uint64(613) << np.uint64(32)
+    keys = np.concatenate([keys, hot | low])
+    perm = g.permutation(keys.size)
+    keys = keys[perm]
+    vals = np.arange(keys.size, dtype=np.uint32)
+    end = 32 + primitives.higher_msb(T)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, end)
+    ko, vo = primitives.sort_pairs(u64(keys), u32(vals), 0, end)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    ko, vo, r = primitives.sort_tile_pairs(u64(keys), u32(vals), T)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
+
+
+def test_several_hot_tiles_back_to_back_calls():
+    """Six hot tiles of 20K-150K pairs at once (records of different sizes sharing the queue), the
+    same scratch reused by consecutive calls (the queue's counters restart each call)."""
+    g = np.random.default_rng(5)
+    T = 2048
+    keys, vals = raster_like_keys(700_000, T, 9)
+    sizes = [20_000, 35_000, 60_000, 90_000, 120_000, 150_000]
+    hot = [((np.uint64(100 + 300 * i) << np.uint64(32)) |
+            g.uniform(0.5, 60.0, s).astype(np.float32).view(np.uint32).astype(np.uint64)) for i, s in enumerate(sizes)]
+    keys = np.concatenate([keys] + hot)[g.permutation(700_000 + sum(sizes))]
+    vals = np.arange(keys.size, dtype=np.uint32)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
+    kd, vd = u64(keys), u32(vals)
+    for _ in range(3):
+        ko, vo, r = primitives.sort_tile_pairs(kd, vd, T)
+        assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+        assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)

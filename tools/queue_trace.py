@@ -1,0 +1,53 @@
+"""Per-job timeline of the per-tile sort's partition queue for one hot tile (experiments only).
+
+Needs a library built with -DHIDEGS_QUEUE_TRACE:
+    python tools/build_variant.py qtrace -DHIDEGS_QUEUE_TRACE=1
+    HIDEGS_LIB=variants/libhidegs_qtrace.so python tools/queue_trace.py [hot_pairs ...]
+Times are wall_clock64 ticks (100 MHz) relative to the first claim, in microseconds."""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from hidegs_amd import _lib, primitives, synthetic  # noqa: E402
+
+NAMES = {1: "SMALL", 2: "COPY", 3: "REDUCE", 4: "HIST", 5: "SCATTER", 6: "GLOBAL"}
+L = _lib.lib()
+fn = L.hidegs_debug_queue_trace
+fn.restype = C.c_int
+fn.argtypes = [C.c_void_p, C.c_int]
+
+wl = synthetic.binning_workload(2_000_000, 1920, 1080, seed=0, device="cuda")
+buf = np.zeros((8192, 4), np.uint64)
+for hot in [int(a) for a in sys.argv[1:]] or [4096, 100_000]:
+    keys = wl.keys.clone()
+    idx = torch.randperm(keys.numel(), device="cuda")[:hot]
+    keys[idx] = (keys[idx] & 0xFFFFFFFF) | (4000 << 32)
+    primitives.sort_tile_pairs(keys, wl.values, wl.num_tiles)
+    torch.cuda.synchronize()
+    fn(buf.ctypes.data, 8192)  # drop the warm-up's trace
+    primitives.sort_tile_pairs(keys, wl.values, wl.num_tiles)
+    n = fn(buf.ctypes.data, 8192)
+    tr = buf[:n].copy()
+    t0 = tr[:, 1].min()
+    rel = (tr[:, 1:].astype(np.int64) - int(t0)) / 100.0
+    order = np.argsort(rel[:, 1])
+    print(f"hot tile {hot} pairs: {n} jobs, last end {rel[:, 2].max():.1f} us")
+    kinds = {}
+    for j in order:
+        ty = int(tr[j, 0] & 0x7F)
+        last = " last" if tr[j, 0] & 0x80 else ""
+        kinds.setdefault(NAMES.get(ty, ty) + last, []).append(rel[j, 2] - rel[j, 1])
+    for k, v in kinds.items():
+        print(f"  {k:13s} x{len(v):4d}: run p50 {np.median(v):7.1f}  p90 {np.percentile(v, 90):7.1f}  max {np.max(v):7.1f} us")
+    wait = rel[:, 1] - rel[:, 0]
+    print(f"  claim->got wait p50 {np.median(wait):.1f} us; jobs started per 20 us:",
+          np.histogram(rel[:, 1], bins=np.arange(0, rel[:, 2].max() + 20, 20))[0].tolist())
+    show = order[:12] if len(order) < 60 else np.argsort(-(rel[:, 2] - rel[:, 1]))[:15]
+    for j in show:
+        ty = int(tr[j, 0] & 0x7F)
+        print(f"  job {int(tr[j, 0] >> 32):5d} {NAMES.get(ty, ty):8s}{'*' if tr[j, 0] & 0x80 else ' '} block "
+              f"{int((tr[j, 0] >> 8) & 0xFFFFFF):4d}  claimed {rel[j, 0]:8.1f}  got {rel[j, 1]:8.1f}  end {rel[j, 2]:8.1f}")
