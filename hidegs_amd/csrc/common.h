@@ -50,6 +50,16 @@ constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// Block b of nb -> a work index such that consecutive work indices run on one XCD: the dispatcher
+// deals workgroups to the 8 XCDs round-robin (b, b+8, ... share an XCD's L2), so this hands each
+// XCD a contiguous range of indices.
+__device__ __forceinline__ int xcd_swizzle(int b, int nb)
+{
+    // consecutive leaf groups land on one XCD (blocks b, b+8, ... share an XCD's L2)
+    const int per = nb / 8, rem = nb % 8, x = b % 8, k = b / 8;
+    return (x < rem) ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_shfl_xor(T v, int m)
 {

@@ -141,13 +141,6 @@ __device__ __forceinline__ void eval_chunk(const float4* stage, int k0, int nval
     }
 }
 
-__device__ __forceinline__ int xcd_swizzle(int b, int nb)
-{
-    // consecutive leaf groups land on one XCD (blocks b, b+8, ... share an XCD's L2)
-    const int per = nb / 8, rem = nb % 8, x = b % 8, k = b / 8;
-    return (x < rem) ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
-}
-
 __device__ __forceinline__ uint64_t spread3(uint32_t v)
 {
     // bit i of v -> bit 3i (v < 2^21)

@@ -272,6 +272,11 @@ __global__ __launch_bounds__(kBlock) void radix_digit_scan_kernel(uint32_t* __re
                                 // of 8 pairs each (66 VGPRs, 6 waves/SIMD) measured 2-3% faster than 4 of 16
 #endif
 constexpr int kSWaves = HIDEGS_SCATTER_WAVES;
+#ifndef HIDEGS_XCD_TILES
+#define HIDEGS_XCD_TILES 1  // neighbouring tiles on one XCD: 46.3 -> 42.9 us per pass at 8M pairs (their
+                            // shared output lines at digit-run ends merge in one L2); the same
+                            // mapping for segment_sort measured 48.1 -> 49.7 us and is not used there
+#endif
 constexpr int kSBlock = kSWaves * kWave;
 constexpr int kSItems = kTile / kSBlock;  // pairs per thread
 static_assert(kSBlock >= kRadix, "one thread per digit in the digit scans");
@@ -296,12 +301,13 @@ __global__ __launch_bounds__(kSBlock) void radix_scatter_kernel(const K* __restr
     const int wave = t / kWave;
     const bool digit_thread = t < kRadix;  // thread d owns digit d in the digit scans
     for (int i = t; i < kSWaves * kRadix; i += kSBlock) (&s_cnt[0][0])[i] = 0;
-    const long long base = (long long)blockIdx.x * kTile;
+    const int tile = HIDEGS_XCD_TILES ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const long long base = (long long)tile * kTile;
     const long long seg = base + (long long)wave * (kSItems * kWave);  // this wave's items
     // this tile's global digit offsets, loaded now so their latency hides behind the ranking (digits
     // above `mask` read stale counts that no item uses)
     const uint32_t digit_total = digit_thread ? totals[t] : 0u;
-    const uint32_t digit_prefix = digit_thread ? tile_prefix[(long long)t * ntiles + blockIdx.x] : 0u;
+    const uint32_t digit_prefix = digit_thread ? tile_prefix[(long long)t * ntiles + tile] : 0u;
 
     K k[kSItems];
     uint32_t v[kSItems];
