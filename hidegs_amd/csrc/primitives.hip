@@ -240,9 +240,13 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const K* __restrict_
 }
 
 // One workgroup per digit: exclusive scan of counts[d][0..ntiles) in place; totals[d] = sum.
+// zero (nzero words, or NULL) is cleared on the side: the segmented sort's range array, which
+// segment_ranges fills next (one memset launch less).
 __global__ __launch_bounds__(kBlock) void radix_digit_scan_kernel(uint32_t* __restrict__ counts, int ntiles,
-                                                                  uint32_t* __restrict__ totals)
+                                                                  uint32_t* __restrict__ totals,
+                                                                  uint32_t* __restrict__ zero, int nzero)
 {
+    for (int j = blockIdx.x * kBlock + threadIdx.x; j < nzero; j += gridDim.x * kBlock) zero[j] = 0u;
     __shared__ uint32_t s_wave[kWavesPerBlock];
     uint32_t* row = counts + (long long)blockIdx.x * ntiles;
     uint32_t carry = 0;
@@ -1763,6 +1767,23 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
     const int lo_bit = segmented ? 32 : begin_bit;
     const int lsd_passes = segmented ? (end_bit - 32 + kRadixBits - 1) / kRadixBits : passes;
 
+    // segmented path: the segment ranges (the caller's tile ranges with ranges_out: tile ids
+    // < num_tiles <= 2^(end_bit-32) leave no bits above end_bit, so segment == tile), cleared by the
+    // last pass's digit scan
+    int nseg = 0;
+    uint2* ranges = nullptr;
+    uint32_t tile_mask = 0u;
+    if (segmented) {
+        nseg = 1 << (end_bit - 32);
+        ranges = c.take<uint2>((size_t)1 << kMaxSegmentBits);
+        tile_mask = (uint32_t)(nseg - 1);
+        if (ranges_out) {
+            ranges = ranges_out;
+            nseg = num_tiles;
+            tile_mask = 0xffffffffu;
+        }
+    }
+
     const K* src_k = keys_in;
     const uint32_t* src_v = vals_in;
     // balanced digit widths (13 tile bits: 7 + 6, not 8 + 5): fewer buckets per pass mean
@@ -1779,8 +1800,9 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
                       dim3(kBlock), 0, stream, src_k, n, shift, mask, nt, counts);
         // digits above `mask` never occur: their (stale) totals only follow the used digits in the
         // scatter's exclusive scan, and their counts are never read
+        const bool clear = segmented && p == lsd_passes - 1;
         HIDEGS_LAUNCH("radix_digit_scan", radix_digit_scan_kernel, dim3(mask + 1), dim3(kBlock), 0, stream, counts,
-                      nt, totals);
+                      nt, totals, clear ? reinterpret_cast<uint32_t*>(ranges) : nullptr, clear ? 2 * nseg : 0);
         HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"), radix_scatter_kernel<K>,
                       dim3(nt), dim3(kSBlock), 0, stream, src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals);
         src_k = dk;
@@ -1788,16 +1810,6 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         shift += bits;
     }
     if (segmented) {
-        // the segments' ranges; with ranges_out they are the caller's tile ranges (tile ids
-        // < num_tiles <= 2^(end_bit-32) leave no bits above end_bit, so segment == tile)
-        int nseg = 1 << (end_bit - 32);
-        uint2* ranges = c.take<uint2>((size_t)1 << kMaxSegmentBits);
-        uint32_t tile_mask = (uint32_t)(nseg - 1);
-        if (ranges_out) {
-            ranges = ranges_out;
-            nseg = num_tiles;
-            tile_mask = 0xffffffffu;
-        }
         BigQueue q = queue_caps(n);
         q.ctl = c.take<uint32_t>(Q_WORDS);
         q.rec = c.take<BigSeg>(q.rec_cap);
@@ -1806,8 +1818,6 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         q.alt_k = reinterpret_cast<uint64_t*>(alt_k);
         q.alt_v = alt_v;
         uint64_t* ko = reinterpret_cast<uint64_t*>(keys_out);
-        if (hipMemsetAsync(ranges, 0, sizeof(uint2) * nseg, stream) != hipSuccess)
-            return fail(HIDEGS_E_HIP, std::string(what) + ": memset failed");
         HIDEGS_LAUNCH("segment_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock * kRangeKeys)), dim3(kBlock), 0, stream,
                       (const uint64_t*)ko, n, ranges, (uint32_t)nseg, tile_mask, q);
         HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out, ranges, q);
