@@ -239,6 +239,10 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const K* __restrict_
     }
 }
 
+#ifndef HIDEGS_DIGIT_ITEMS
+#define HIDEGS_DIGIT_ITEMS 8
+#endif
+constexpr int kDigitItems = HIDEGS_DIGIT_ITEMS;
 // One workgroup per digit: exclusive scan of counts[d][0..ntiles) in place; totals[d] = sum.
 // zero (nzero words, or NULL) is cleared on the side: the segmented sort's range array, which
 // segment_ranges fills next (one memset launch less).
@@ -249,21 +253,22 @@ __global__ __launch_bounds__(kBlock) void radix_digit_scan_kernel(uint32_t* __re
     for (int j = blockIdx.x * kBlock + threadIdx.x; j < nzero; j += gridDim.x * kBlock) zero[j] = 0u;
     __shared__ uint32_t s_wave[kWavesPerBlock];
     uint32_t* row = counts + (long long)blockIdx.x * ntiles;
+    // HIDEGS_DIGIT_ITEMS per thread: one round (one memory latency) for up to 256 x that many tiles
     uint32_t carry = 0;
-    for (int base = 0; base < ntiles; base += kBlock * 4) {
-        uint32_t v[4];
+    for (int base = 0; base < ntiles; base += kBlock * kDigitItems) {
+        uint32_t v[kDigitItems];
         uint32_t sum = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            int i = base + threadIdx.x * 4 + j;
+        for (int j = 0; j < kDigitItems; j++) {
+            int i = base + threadIdx.x * kDigitItems + j;
             v[j] = (i < ntiles) ? row[i] : 0u;
             sum += v[j];
         }
         uint32_t total;
         uint32_t pre = block_exclusive_scan(sum, s_wave, &total) + carry;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            int i = base + threadIdx.x * 4 + j;
+        for (int j = 0; j < kDigitItems; j++) {
+            int i = base + threadIdx.x * kDigitItems + j;
             if (i < ntiles) row[i] = pre;
             pre += v[j];
         }
