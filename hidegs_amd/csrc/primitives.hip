@@ -193,10 +193,14 @@ __device__ __forceinline__ uint32_t digit_wave_prefix(uint32_t (*s_cnt)[kRadix])
 #define HIDEGS_XCD_HIST 1  // 16.4 -> 13.5 us per pass at 8M keys (A/B builds: 0)
 #endif
 // counts[d * ntiles + tile] = number of keys of tile `tile` whose digit is d.
+// zero_jobs: zero_count 16-byte slots cleared on the side (the hot-tile queue's job slots).
 template <typename K>
 __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const K* __restrict__ keys, long long n, int shift,
-                                                            uint32_t mask, int ntiles, uint32_t* __restrict__ counts)
+                                                            uint32_t mask, int ntiles, uint32_t* __restrict__ counts,
+                                                            uint4* __restrict__ zero_jobs, uint32_t zero_count)
 {
+    for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < zero_count; j += gridDim.x * kBlock)
+        zero_jobs[j] = make_uint4(0u, 0u, 0u, 0u);
     __shared__ uint32_t s_hist[kWavesPerBlock][kRadix];
     const int t = threadIdx.x;
     const int wave = t / kWave;
@@ -244,13 +248,9 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const K* __restrict_
 #endif
 constexpr int kDigitItems = HIDEGS_DIGIT_ITEMS;
 // One workgroup per digit: exclusive scan of counts[d][0..ntiles) in place; totals[d] = sum.
-// zero (nzero words, or NULL) is cleared on the side: the segmented sort's range array, which
-// segment_ranges fills next (one memset launch less).
 __global__ __launch_bounds__(kBlock) void radix_digit_scan_kernel(uint32_t* __restrict__ counts, int ntiles,
-                                                                  uint32_t* __restrict__ totals,
-                                                                  uint32_t* __restrict__ zero, int nzero)
+                                                                  uint32_t* __restrict__ totals)
 {
-    for (int j = blockIdx.x * kBlock + threadIdx.x; j < nzero; j += gridDim.x * kBlock) zero[j] = 0u;
     __shared__ uint32_t s_wave[kWavesPerBlock];
     uint32_t* row = counts + (long long)blockIdx.x * ntiles;
     // HIDEGS_DIGIT_ITEMS per thread: one round (one memory latency) for up to 256 x that many tiles
@@ -1641,13 +1641,8 @@ constexpr int kRangeKeys = 4;
 // Q_WORDS counters and its job_cap slots (slot tags read 0 until published).
 __global__ __launch_bounds__(kBlock) void identify_ranges_kernel(const uint64_t* __restrict__ keys, long long n,
                                                                  uint2* __restrict__ ranges, uint32_t num_tiles,
-                                                                 uint32_t tile_mask, const BigQueue zero)
+                                                                 uint32_t tile_mask)
 {
-    if (zero.ctl) {
-        if (blockIdx.x == 0 && threadIdx.x < Q_WORDS) zero.ctl[threadIdx.x] = 0u;
-        for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < zero.job_cap; j += gridDim.x * kBlock)
-            zero.job[j] = make_uint4(0u, 0u, 0u, 0u);
-    }
     const long long i0 = ((long long)blockIdx.x * kBlock + threadIdx.x) * kRangeKeys;
     if (i0 >= n) return;
     uint32_t tile[kRangeKeys];
@@ -1681,7 +1676,79 @@ __global__ __launch_bounds__(kBlock) void identify_ranges_kernel(const uint64_t*
     }
 }
 
+// The segments' ranges from the tile-bit passes' digit counts, without a pass over the sorted keys.
+// Pass 0 sorts by the low segment bits L (b0 of them), pass 1 by the high ones H (b1; 0 = one pass).
+// In pass 1's input (pass 0's output, `mid_keys`) segment L occupies [p0, p1) = [base0[L],
+// base0[L] + T0[L]); pass 1 is stable, so segment (H, L) starts at base1[H] plus the number of
+// digit-H keys before p0 in that input: prefix1[H][p0 / kTile] (the digit scan's per-tile prefix)
+// plus the digit-H keys of p0's own tile before p0 (counted here: < kTile keys).  Workgroup L
+// counts them for p0 and p1 and writes ranges[(H << b0) | L] for every H -- (0, 0) for an empty
+// segment, as identify_tile_ranges leaves it.  It also resets the hot-tile queue's counters.
+__global__ __launch_bounds__(kBlock) void segment_ranges_kernel(const uint64_t* __restrict__ mid_keys, long long n,
+                                                                int b0, int b1, const uint32_t* __restrict__ totals0,
+                                                                const uint32_t* __restrict__ totals1,
+                                                                const uint32_t* __restrict__ prefix1, int ntiles,
+                                                                uint2* __restrict__ ranges, int nseg,
+                                                                uint32_t* __restrict__ ctl)
+{
+    __shared__ uint32_t s_wave[kWavesPerBlock];
+    __shared__ uint32_t s_hist[2][kRadix];
+    __shared__ uint32_t s_p[2];
+    const int t = threadIdx.x;
+    const uint32_t L = blockIdx.x;
+    if (ctl && L == 0 && t < Q_WORDS) ctl[t] = 0u;
+    const uint32_t mask1 = b1 ? (1u << b1) - 1u : 0u;
+    // every load that does not depend on p0 / p1 first (one memory latency for all of them)
+    const uint32_t t0 = t < (1 << b0) ? totals0[t] : 0u;  // b0 <= 8: one thread per low digit
+    const uint32_t t1 = b1 && (uint32_t)t <= mask1 ? totals1[t] : 0u;
+    s_hist[0][t] = 0u;
+    s_hist[1][t] = 0u;
+    uint32_t dummy;
+    const uint32_t base0 = block_exclusive_scan(t0, s_wave, &dummy);
+    const uint32_t base1 = block_exclusive_scan(t1, s_wave, &dummy);
+    if ((uint32_t)t == L) {
+        s_p[0] = base0;
+        s_p[1] = base0 + t0;
+    }
+    __syncthreads();
+    const uint32_t p0 = s_p[0], p1 = s_p[1];
+    if (b1 == 0) {  // one pass: segment L is [p0, p1)
+        if (t == 0 && (int)L < nseg) ranges[L] = p1 > p0 ? make_uint2(p0, p1) : make_uint2(0u, 0u);
+        return;
+    }
+    // then the per-tile prefixes and the keys before p0 / p1 in their tiles, together
+    const uint32_t H = (uint32_t)t;
+    const bool own = H <= mask1;
+    const uint32_t q0 = own && (long long)p0 < n ? prefix1[(long long)H * ntiles + (p0 / kTile)] : t1;
+    const uint32_t q1 = own && (long long)p1 < n ? prefix1[(long long)H * ntiles + (p1 / kTile)] : t1;
+    const int shift1 = 32 + b0;
+    uint32_t d[2][kItems];
+#pragma unroll
+    for (int w = 0; w < 2; w++) {
+        const uint32_t p = w ? p1 : p0;
+        const uint32_t r = (long long)p < n ? p & (kTile - 1) : 0u;  // keys of p's tile before p
+        const long long tb = (long long)(p - r);
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            const uint32_t i = (uint32_t)t + j * kBlock;
+            d[w][j] = i < r ? (uint32_t)(mid_keys[tb + i] >> shift1) & mask1 : ~0u;
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < 2; w++)
+#pragma unroll
+        for (int j = 0; j < kItems; j++)
+            if (d[w][j] != ~0u) atomicAdd(&s_hist[w][d[w][j]], 1u);
+    __syncthreads();
+    if (own) {
+        const uint32_t c0 = q0 + s_hist[0][H], c1 = q1 + s_hist[1][H];
+        const uint32_t seg = (H << b0) | L;
+        if ((int)seg < nseg) ranges[seg] = c1 > c0 ? make_uint2(base1 + c0, base1 + c1) : make_uint2(0u, 0u);
+    }
+}
+
 // ============================== host side ======================================
+
 
 size_t scan_scratch(long long n)
 {
@@ -1716,7 +1783,7 @@ size_t sort_scratch(long long n)
 {
     const int nt = ceil_div(n, kTile);
     size_t b = align_up((size_t)n * sizeof(K)) + align_up((size_t)n * sizeof(uint32_t)) +
-               align_up((size_t)kRadix * nt * sizeof(uint32_t)) + align_up(kRadix * sizeof(uint32_t));
+               align_up((size_t)kRadix * nt * sizeof(uint32_t)) + 2 * align_up(kRadix * sizeof(uint32_t));
     if (sizeof(K) == 8) {  // segmented path: the segment ranges and the partition queue
         const BigQueue q = queue_caps(n);
         b += align_up(sizeof(uint2) << kMaxSegmentBits) + align_up(Q_WORDS * sizeof(uint32_t)) +
@@ -1727,7 +1794,11 @@ size_t sort_scratch(long long n)
 }
 
 __global__ void identify_ranges_kernel(const uint64_t* __restrict__ keys, long long n, uint2* __restrict__ ranges,
-                                       uint32_t num_tiles, uint32_t tile_mask, const BigQueue zero);
+                                       uint32_t num_tiles, uint32_t tile_mask);
+__global__ void segment_ranges_kernel(const uint64_t* __restrict__ mid_keys, long long n, int b0, int b1,
+                                      const uint32_t* __restrict__ totals0, const uint32_t* __restrict__ totals1,
+                                      const uint32_t* __restrict__ prefix1, int ntiles, uint2* __restrict__ ranges,
+                                      int nseg, uint32_t* __restrict__ ctl);
 
 // ranges_out (num_tiles entries) set: the tile ranges of the sorted keys are written too, with
 // identify_tile_ranges' semantics; the caller guarantees key >> 32 < num_tiles.
@@ -1764,7 +1835,7 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
     K* alt_k = c.take<K>(n);
     uint32_t* alt_v = c.take<uint32_t>(n);
     uint32_t* counts = c.take<uint32_t>((size_t)kRadix * nt);
-    uint32_t* totals = c.take<uint32_t>(kRadix);
+    uint32_t* totals_pass[2] = {c.take<uint32_t>(kRadix), c.take<uint32_t>(kRadix)};  // alternate passes
 
     // (tile | depth)-shaped sort: LSD over the segment bits only, then per-segment LDS sorts
     const bool segmented = sizeof(K) == 8 && begin_bit == 0 && end_bit > 32 && end_bit - 32 <= kMaxSegmentBits &&
@@ -1773,20 +1844,25 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
     const int lsd_passes = segmented ? (end_bit - 32 + kRadixBits - 1) / kRadixBits : passes;
 
     // segmented path: the segment ranges (the caller's tile ranges with ranges_out: tile ids
-    // < num_tiles <= 2^(end_bit-32) leave no bits above end_bit, so segment == tile), cleared by the
-    // last pass's digit scan
+    // < num_tiles <= 2^(end_bit-32) leave no bits above end_bit, so segment == tile) and the
+    // hot-tile queue (its job slots are cleared by the last histogram pass)
     int nseg = 0;
     uint2* ranges = nullptr;
-    uint32_t tile_mask = 0u;
+    BigQueue q{};
     if (segmented) {
         nseg = 1 << (end_bit - 32);
         ranges = c.take<uint2>((size_t)1 << kMaxSegmentBits);
-        tile_mask = (uint32_t)(nseg - 1);
         if (ranges_out) {
             ranges = ranges_out;
             nseg = num_tiles;
-            tile_mask = 0xffffffffu;
         }
+        q = queue_caps(n);
+        q.ctl = c.take<uint32_t>(Q_WORDS);
+        q.rec = c.take<BigSeg>(q.rec_cap);
+        q.job = c.take<uint4>(q.job_cap);
+        q.pool = c.take<uint32_t>(q.pool_cap);
+        q.alt_k = reinterpret_cast<uint64_t*>(alt_k);
+        q.alt_v = alt_v;
     }
 
     const K* src_k = keys_in;
@@ -1795,19 +1871,33 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
     // longer runs per bucket in each tile's scatter, i.e. fuller write lines
     const int span = end_bit - lo_bit;
     int shift = lo_bit;
+    int pass_bits[2] = {0, 0};
     for (int p = 0; p < lsd_passes; p++) {
         const int bits = (span * (p + 1)) / lsd_passes - (span * p) / lsd_passes;
         const uint32_t mask = (1u << bits) - 1u;
         const bool to_out = ((lsd_passes - 1 - p) % 2) == 0;
         K* dk = to_out ? keys_out : alt_k;
         uint32_t* dv = to_out ? vals_out : alt_v;
+        uint32_t* totals = totals_pass[p & 1];
+        const bool last = p == lsd_passes - 1;
+        uint4* zero_jobs = segmented && last ? q.job : nullptr;
         HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_hist_u64" : "radix_hist_u32"), radix_hist_kernel<K>, dim3(nt),
-                      dim3(kBlock), 0, stream, src_k, n, shift, mask, nt, counts);
+                      dim3(kBlock), 0, stream, src_k, n, shift, mask, nt, counts, zero_jobs,
+                      zero_jobs ? q.job_cap : 0u);
         // digits above `mask` never occur: their (stale) totals only follow the used digits in the
         // scatter's exclusive scan, and their counts are never read
-        const bool clear = segmented && p == lsd_passes - 1;
         HIDEGS_LAUNCH("radix_digit_scan", radix_digit_scan_kernel, dim3(mask + 1), dim3(kBlock), 0, stream, counts,
-                      nt, totals, clear ? reinterpret_cast<uint32_t*>(ranges) : nullptr, clear ? 2 * nseg : 0);
+                      nt, totals);
+        if (p < 2) pass_bits[p] = bits;
+        if (segmented && last) {
+            // the segments' ranges from the passes' digit counts (no pass over the sorted keys).  (Run
+            // on a side stream beside this scatter, which it could overlap, the fork / join events
+            // cost more than the kernel: 0.180 -> 0.198 ms per binning step.)
+            const int b0 = pass_bits[0], b1 = lsd_passes == 2 ? pass_bits[1] : 0;
+            HIDEGS_LAUNCH("segment_ranges", segment_ranges_kernel, dim3(1u << b0), dim3(kBlock), 0, stream,
+                          reinterpret_cast<const uint64_t*>(lsd_passes == 2 ? alt_k : keys_in), n, b0, b1,
+                          totals_pass[0], totals_pass[1], counts, nt, ranges, nseg, q.ctl);
+        }
         HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"), radix_scatter_kernel<K>,
                       dim3(nt), dim3(kSBlock), 0, stream, src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals);
         src_k = dk;
@@ -1815,16 +1905,7 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         shift += bits;
     }
     if (segmented) {
-        BigQueue q = queue_caps(n);
-        q.ctl = c.take<uint32_t>(Q_WORDS);
-        q.rec = c.take<BigSeg>(q.rec_cap);
-        q.job = c.take<uint4>(q.job_cap);
-        q.pool = c.take<uint32_t>(q.pool_cap);
-        q.alt_k = reinterpret_cast<uint64_t*>(alt_k);
-        q.alt_v = alt_v;
         uint64_t* ko = reinterpret_cast<uint64_t*>(keys_out);
-        HIDEGS_LAUNCH("segment_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock * kRangeKeys)), dim3(kBlock), 0, stream,
-                      (const uint64_t*)ko, n, ranges, (uint32_t)nseg, tile_mask, q);
         HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out, ranges, q);
         HIDEGS_LAUNCH("big_segments", big_segment_kernel, dim3(kQueueBlocks), dim3(kBlock), 0, stream, ko, vals_out,
                       reinterpret_cast<uint64_t*>(alt_k), alt_v, q);
@@ -1891,7 +1972,7 @@ int identify_tile_ranges(const uint64_t* keys, long long n, uint32_t* ranges, in
     if (n == 0) return check_launch("identify_tile_ranges", stream, 0);
     if (!keys) return fail(HIDEGS_E_ARG, "identify_tile_ranges: NULL keys");
     HIDEGS_LAUNCH("identify_ranges", identify_ranges_kernel, dim3(ceil_div(n, kBlock * kRangeKeys)), dim3(kBlock), 0, stream, keys, n,
-                       reinterpret_cast<uint2*>(ranges), (uint32_t)num_tiles, 0xffffffffu, BigQueue{});
+                       reinterpret_cast<uint2*>(ranges), (uint32_t)num_tiles, 0xffffffffu);
     return check_launch("identify_tile_ranges", stream, 0);
 }
 
