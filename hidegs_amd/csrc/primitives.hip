@@ -248,9 +248,19 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const K* __restrict_
 #endif
 constexpr int kDigitItems = HIDEGS_DIGIT_ITEMS;
 // One workgroup per digit: exclusive scan of counts[d][0..ntiles) in place; totals[d] = sum.
+// low_totals (nlow <= 256 digit totals of the previous pass, or NULL): workgroup 0 also writes
+// their exclusive scan to low_base (the segment starts of radix_scatter_kernel<K, true>).
 __global__ __launch_bounds__(kBlock) void radix_digit_scan_kernel(uint32_t* __restrict__ counts, int ntiles,
-                                                                  uint32_t* __restrict__ totals)
+                                                                  uint32_t* __restrict__ totals,
+                                                                  const uint32_t* __restrict__ low_totals, int nlow,
+                                                                  uint32_t* __restrict__ low_base)
 {
+    if (low_totals && blockIdx.x == 0) {
+        __shared__ uint32_t s_low[kWavesPerBlock];
+        uint32_t dummy;
+        const uint32_t b = block_exclusive_scan((int)threadIdx.x < nlow ? low_totals[threadIdx.x] : 0u, s_low, &dummy);
+        if ((int)threadIdx.x < nlow) low_base[threadIdx.x] = b;
+    }
     __shared__ uint32_t s_wave[kWavesPerBlock];
     uint32_t* row = counts + (long long)blockIdx.x * ntiles;
     // HIDEGS_DIGIT_ITEMS per thread: one round (one memory latency) for up to 256 x that many tiles
@@ -296,13 +306,64 @@ constexpr int kSBlock = kSWaves * kWave;
 constexpr int kSItems = kTile / kSBlock;  // pairs per thread
 static_assert(kSBlock >= kRadix, "one thread per digit in the digit scans");
 
-template <typename K>
+// radix_scatter_kernel<K, true>'s segment starts (see there); every thread of the workgroup calls it.
+template <typename K, int R>
+__device__ __forceinline__ void segment_starts(const K (&k)[R], const bool (&ok)[R], const int shift, const uint32_t mask,
+                                            const long long n, const int tile, const int ntiles,
+                                            const long long base, const uint32_t digit_base,
+                                            const uint32_t p0, const int b0, uint32_t* starts)
+{
+    __shared__ uint32_t s_bhist[kRadix];
+    __shared__ uint32_t s_blist[kRadix];
+    __shared__ uint32_t s_nb;
+    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
+    if (t == 0) {
+        s_nb = 0u;
+        if (tile == 0) starts[(mask + 1u) << b0] = (uint32_t)n;
+    }
+    if (b0 == 0) {  // one pass: the digit bases of tile 0 are the segment starts
+        if (tile == 0 && t <= (int)mask) starts[t] = digit_base;
+        return;
+    }
+    __syncthreads();  // s_nb
+    // low values whose first position p0 = base0[t] lies in this tile (position n: the last tile)
+    if (t < (1 << b0) && (((long long)p0 >= base && (long long)p0 < base + kTile) ||
+                          ((long long)p0 >= n && tile == ntiles - 1)))
+        s_blist[atomicAdd(&s_nb, 1u)] = (uint32_t)t | (((uint32_t)((long long)p0 - base)) << 8);
+    __syncthreads();
+    const uint32_t nb = s_nb;  // workgroup-uniform; 0 for most tiles
+    for (uint32_t b = 0; b < nb; b++) {
+        const uint32_t e = s_blist[b], L = e & 0xffu, r = e >> 8;  // the tile's pairs [0, r) precede L
+        if (t < kRadix) s_bhist[t] = 0u;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            const uint32_t li = (uint32_t)(wave * (R * kWave) + q * kWave + lane);
+            if (ok[q] && li < r) atomicAdd(&s_bhist[digit_of(k[q], shift, mask)], 1u);
+        }
+        __syncthreads();
+        if (t <= (int)mask) starts[((uint32_t)t << b0) | L] = digit_base + s_bhist[t];
+        __syncthreads();
+    }
+}
+
+// Starts (the segmented sort's last segment-bit pass): also the output position of each segment's
+// first pair, starts[(H << b0) | L] for segment (H = this pass's digit, L = the b0 segment bits of
+// the pass before), so that no kernel has to find the ranges in the sorted keys.  Pass 1 is stable
+// and its input is ordered by L: segment (H, L) starts at this tile's global base of digit H plus
+// the digit-H pairs of this tile that precede base0[L] (the first input position of L: the
+// exclusive scan of pass 0's digit totals, totals0), for the tile that holds base0[L].  b0 == 0
+// (one pass, the digit is the whole segment id): tile 0 writes starts[d] = base of digit d.
+// starts[(mask + 1) << b0] = n closes the last segment.
+template <typename K, bool Starts = false>
 __global__ __launch_bounds__(kSBlock) void radix_scatter_kernel(const K* __restrict__ keys_in,
                                                                 const uint32_t* __restrict__ vals_in,
                                                                 K* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
                                                                 long long n, int shift, uint32_t mask, int ntiles,
                                                                 const uint32_t* __restrict__ tile_prefix,
-                                                                const uint32_t* __restrict__ totals)
+                                                                const uint32_t* __restrict__ totals,
+                                                                const uint32_t* __restrict__ totals0, int b0,
+                                                                uint32_t* __restrict__ starts)
 {
     __shared__ __attribute__((aligned(16))) K s_stage[kTile];  // keys by tile-local rank, then values
     __shared__ uint32_t s_cnt[kSWaves][kRadix];         // per-wave running counters
@@ -323,6 +384,7 @@ __global__ __launch_bounds__(kSBlock) void radix_scatter_kernel(const K* __restr
     // above `mask` read stale counts that no item uses)
     const uint32_t digit_total = digit_thread ? totals[t] : 0u;
     const uint32_t digit_prefix = digit_thread ? tile_prefix[(long long)t * ntiles + tile] : 0u;
+    const uint32_t low_base = Starts && b0 > 0 && t < (1 << b0) ? totals0[t] : 0u;  // base0[t]; b0 <= 8
 
     K k[kSItems];
     uint32_t v[kSItems];
@@ -338,6 +400,8 @@ __global__ __launch_bounds__(kSBlock) void radix_scatter_kernel(const K* __restr
     // do not wait for global loads)
     uint32_t dummy;
     const uint32_t digit_base = block_exclusive_scan<kSWaves>(digit_total, s_wave, &dummy) + digit_prefix;
+    // (at the end of the kernel instead, with the keys kept live: 73 VGPRs against 61, same time)
+    if (Starts) segment_starts(k, ok, shift, mask, n, tile, ntiles, base, digit_base, low_base, b0, starts);
     uint32_t rank[kSItems];
     wave_rank<K, kSItems>(k, ok, shift, mask, s_cnt[wave], rank, mask);
     __syncthreads();
@@ -1217,11 +1281,15 @@ __device__ __forceinline__ void open_local(const uint64_t* keys, const BigQueue&
 // Workgroup b sorts segment b in place by the low 32 key bits (sort_segment); a segment of more
 // than kSegCap pairs becomes a record of the partition queue (big_segment_kernel runs it).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_SEG_WAVES))) void segment_sort_kernel(
-    uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint2* __restrict__ ranges, const BigQueue q)
+    uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint32_t* __restrict__ starts,
+    uint2* __restrict__ ranges_out, const BigQueue q)
 {
     __shared__ __attribute__((aligned(16))) SegLds lds;
     __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock], s_max[kWavesPerBlock];
-    const uint2 r = ranges[blockIdx.x];
+    // segment b is [starts[b], starts[b + 1]); with ranges_out it is also tile b's range, (0, 0) when
+    // empty -- identifyTileRanges' result
+    const uint2 r = make_uint2(starts[blockIdx.x], starts[blockIdx.x + 1]);
+    if (ranges_out && threadIdx.x == 0) ranges_out[blockIdx.x] = r.y > r.x ? r : make_uint2(0u, 0u);
     const uint32_t begin = r.x, m = r.y - r.x;
     if (r.y <= r.x + 1) return;  // absent or single pair: already in place
     if (m > (uint32_t)kSegCap) {
@@ -1676,77 +1744,6 @@ __global__ __launch_bounds__(kBlock) void identify_ranges_kernel(const uint64_t*
     }
 }
 
-// The segments' ranges from the tile-bit passes' digit counts, without a pass over the sorted keys.
-// Pass 0 sorts by the low segment bits L (b0 of them), pass 1 by the high ones H (b1; 0 = one pass).
-// In pass 1's input (pass 0's output, `mid_keys`) segment L occupies [p0, p1) = [base0[L],
-// base0[L] + T0[L]); pass 1 is stable, so segment (H, L) starts at base1[H] plus the number of
-// digit-H keys before p0 in that input: prefix1[H][p0 / kTile] (the digit scan's per-tile prefix)
-// plus the digit-H keys of p0's own tile before p0 (counted here: < kTile keys).  Workgroup L
-// counts them for p0 and p1 and writes ranges[(H << b0) | L] for every H -- (0, 0) for an empty
-// segment, as identify_tile_ranges leaves it.  It also resets the hot-tile queue's counters.
-__global__ __launch_bounds__(kBlock) void segment_ranges_kernel(const uint64_t* __restrict__ mid_keys, long long n,
-                                                                int b0, int b1, const uint32_t* __restrict__ totals0,
-                                                                const uint32_t* __restrict__ totals1,
-                                                                const uint32_t* __restrict__ prefix1, int ntiles,
-                                                                uint2* __restrict__ ranges, int nseg,
-                                                                uint32_t* __restrict__ ctl)
-{
-    __shared__ uint32_t s_wave[kWavesPerBlock];
-    __shared__ uint32_t s_hist[2][kRadix];
-    __shared__ uint32_t s_p[2];
-    const int t = threadIdx.x;
-    const uint32_t L = blockIdx.x;
-    if (ctl && L == 0 && t < Q_WORDS) ctl[t] = 0u;
-    const uint32_t mask1 = b1 ? (1u << b1) - 1u : 0u;
-    // every load that does not depend on p0 / p1 first (one memory latency for all of them)
-    const uint32_t t0 = t < (1 << b0) ? totals0[t] : 0u;  // b0 <= 8: one thread per low digit
-    const uint32_t t1 = b1 && (uint32_t)t <= mask1 ? totals1[t] : 0u;
-    s_hist[0][t] = 0u;
-    s_hist[1][t] = 0u;
-    uint32_t dummy;
-    const uint32_t base0 = block_exclusive_scan(t0, s_wave, &dummy);
-    const uint32_t base1 = block_exclusive_scan(t1, s_wave, &dummy);
-    if ((uint32_t)t == L) {
-        s_p[0] = base0;
-        s_p[1] = base0 + t0;
-    }
-    __syncthreads();
-    const uint32_t p0 = s_p[0], p1 = s_p[1];
-    if (b1 == 0) {  // one pass: segment L is [p0, p1)
-        if (t == 0 && (int)L < nseg) ranges[L] = p1 > p0 ? make_uint2(p0, p1) : make_uint2(0u, 0u);
-        return;
-    }
-    // then the per-tile prefixes and the keys before p0 / p1 in their tiles, together
-    const uint32_t H = (uint32_t)t;
-    const bool own = H <= mask1;
-    const uint32_t q0 = own && (long long)p0 < n ? prefix1[(long long)H * ntiles + (p0 / kTile)] : t1;
-    const uint32_t q1 = own && (long long)p1 < n ? prefix1[(long long)H * ntiles + (p1 / kTile)] : t1;
-    const int shift1 = 32 + b0;
-    uint32_t d[2][kItems];
-#pragma unroll
-    for (int w = 0; w < 2; w++) {
-        const uint32_t p = w ? p1 : p0;
-        const uint32_t r = (long long)p < n ? p & (kTile - 1) : 0u;  // keys of p's tile before p
-        const long long tb = (long long)(p - r);
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-            const uint32_t i = (uint32_t)t + j * kBlock;
-            d[w][j] = i < r ? (uint32_t)(mid_keys[tb + i] >> shift1) & mask1 : ~0u;
-        }
-    }
-#pragma unroll
-    for (int w = 0; w < 2; w++)
-#pragma unroll
-        for (int j = 0; j < kItems; j++)
-            if (d[w][j] != ~0u) atomicAdd(&s_hist[w][d[w][j]], 1u);
-    __syncthreads();
-    if (own) {
-        const uint32_t c0 = q0 + s_hist[0][H], c1 = q1 + s_hist[1][H];
-        const uint32_t seg = (H << b0) | L;
-        if ((int)seg < nseg) ranges[seg] = c1 > c0 ? make_uint2(base1 + c0, base1 + c1) : make_uint2(0u, 0u);
-    }
-}
-
 // ============================== host side ======================================
 
 
@@ -1786,7 +1783,8 @@ size_t sort_scratch(long long n)
                align_up((size_t)kRadix * nt * sizeof(uint32_t)) + 2 * align_up(kRadix * sizeof(uint32_t));
     if (sizeof(K) == 8) {  // segmented path: the segment ranges and the partition queue
         const BigQueue q = queue_caps(n);
-        b += align_up(sizeof(uint2) << kMaxSegmentBits) + align_up(Q_WORDS * sizeof(uint32_t)) +
+        b += align_up(sizeof(uint32_t) * (((size_t)1 << kMaxSegmentBits) + 1)) + align_up(kRadix * sizeof(uint32_t)) +
+             align_up(Q_WORDS * sizeof(uint32_t)) +
              align_up((size_t)q.rec_cap * sizeof(BigSeg)) + align_up((size_t)q.job_cap * sizeof(uint4)) +
              align_up((size_t)q.pool_cap * sizeof(uint32_t));
     }
@@ -1795,10 +1793,6 @@ size_t sort_scratch(long long n)
 
 __global__ void identify_ranges_kernel(const uint64_t* __restrict__ keys, long long n, uint2* __restrict__ ranges,
                                        uint32_t num_tiles, uint32_t tile_mask);
-__global__ void segment_ranges_kernel(const uint64_t* __restrict__ mid_keys, long long n, int b0, int b1,
-                                      const uint32_t* __restrict__ totals0, const uint32_t* __restrict__ totals1,
-                                      const uint32_t* __restrict__ prefix1, int ntiles, uint2* __restrict__ ranges,
-                                      int nseg, uint32_t* __restrict__ ctl);
 
 // ranges_out (num_tiles entries) set: the tile ranges of the sorted keys are written too, with
 // identify_tile_ranges' semantics; the caller guarantees key >> 32 < num_tiles.
@@ -1847,19 +1841,17 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
     // < num_tiles <= 2^(end_bit-32) leave no bits above end_bit, so segment == tile) and the
     // hot-tile queue (its job slots are cleared by the last histogram pass)
     int nseg = 0;
-    uint2* ranges = nullptr;
+    uint32_t* seg_starts = nullptr;
+    uint32_t* low_base = nullptr;
     BigQueue q{};
     if (segmented) {
-        nseg = 1 << (end_bit - 32);
-        ranges = c.take<uint2>((size_t)1 << kMaxSegmentBits);
-        if (ranges_out) {
-            ranges = ranges_out;
-            nseg = num_tiles;
-        }
+        nseg = ranges_out ? num_tiles : 1 << (end_bit - 32);
+        seg_starts = c.take<uint32_t>(((size_t)1 << kMaxSegmentBits) + 1);
+        low_base = c.take<uint32_t>(kRadix);
         q = queue_caps(n);
-        q.ctl = c.take<uint32_t>(Q_WORDS);
+        q.ctl = c.take<uint32_t>(Q_WORDS);  // the counters and the job slots are contiguous (1 KB + ...):
+        q.job = c.take<uint4>(q.job_cap);   // the last histogram pass clears them as one range
         q.rec = c.take<BigSeg>(q.rec_cap);
-        q.job = c.take<uint4>(q.job_cap);
         q.pool = c.take<uint32_t>(q.pool_cap);
         q.alt_k = reinterpret_cast<uint64_t*>(alt_k);
         q.alt_v = alt_v;
@@ -1880,33 +1872,33 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         uint32_t* dv = to_out ? vals_out : alt_v;
         uint32_t* totals = totals_pass[p & 1];
         const bool last = p == lsd_passes - 1;
-        uint4* zero_jobs = segmented && last ? q.job : nullptr;
+        uint4* zero_jobs = segmented && last ? reinterpret_cast<uint4*>(q.ctl) : nullptr;
+        static_assert(Q_WORDS * sizeof(uint32_t) % kAlign == 0, "ctl and job slots contiguous");
         HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_hist_u64" : "radix_hist_u32"), radix_hist_kernel<K>, dim3(nt),
                       dim3(kBlock), 0, stream, src_k, n, shift, mask, nt, counts, zero_jobs,
-                      zero_jobs ? q.job_cap : 0u);
+                      zero_jobs ? q.job_cap + Q_WORDS / 4 : 0u);
         // digits above `mask` never occur: their (stale) totals only follow the used digits in the
         // scatter's exclusive scan, and their counts are never read
+        const bool low = segmented && last && lsd_passes == 2;  // the previous pass's digit bases, for the starts
         HIDEGS_LAUNCH("radix_digit_scan", radix_digit_scan_kernel, dim3(mask + 1), dim3(kBlock), 0, stream, counts,
-                      nt, totals);
+                      nt, totals, low ? totals_pass[0] : nullptr, low ? 1 << pass_bits[0] : 0, low_base);
         if (p < 2) pass_bits[p] = bits;
-        if (segmented && last) {
-            // the segments' ranges from the passes' digit counts (no pass over the sorted keys).  (Run
-            // on a side stream beside this scatter, which it could overlap, the fork / join events
-            // cost more than the kernel: 0.180 -> 0.198 ms per binning step.)
-            const int b0 = pass_bits[0], b1 = lsd_passes == 2 ? pass_bits[1] : 0;
-            HIDEGS_LAUNCH("segment_ranges", segment_ranges_kernel, dim3(1u << b0), dim3(kBlock), 0, stream,
-                          reinterpret_cast<const uint64_t*>(lsd_passes == 2 ? alt_k : keys_in), n, b0, b1,
-                          totals_pass[0], totals_pass[1], counts, nt, ranges, nseg, q.ctl);
-        }
-        HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"), radix_scatter_kernel<K>,
-                      dim3(nt), dim3(kSBlock), 0, stream, src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals);
+        if (segmented && last)  // also the segments' first positions (no pass over the sorted keys)
+            HIDEGS_LAUNCH("radix_scatter_u64", (radix_scatter_kernel<K, true>), dim3(nt), dim3(kSBlock), 0, stream,
+                          src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals, low_base,
+                          lsd_passes == 2 ? pass_bits[0] : 0, seg_starts);
+        else
+            HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"), (radix_scatter_kernel<K, false>),
+                          dim3(nt), dim3(kSBlock), 0, stream, src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals,
+                          nullptr, 0, nullptr);
         src_k = dk;
         src_v = dv;
         shift += bits;
     }
     if (segmented) {
         uint64_t* ko = reinterpret_cast<uint64_t*>(keys_out);
-        HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out, ranges, q);
+        HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out,
+                      seg_starts, ranges_out, q);
         HIDEGS_LAUNCH("big_segments", big_segment_kernel, dim3(kQueueBlocks), dim3(kBlock), 0, stream, ko, vals_out,
                       reinterpret_cast<uint64_t*>(alt_k), alt_v, q);
     } else if (ranges_out) {

@@ -7,7 +7,9 @@ import torch  # noqa: E402
 
 from hidegs_amd import _lib, primitives, synthetic  # noqa: E402
 
-wl = synthetic.binning_workload(2_000_000, 1920, 1080, seed=0, device="cuda")
+big = len(sys.argv) > 1 and sys.argv[1] == "4k"  # config 5's frame: 10M Gaussians at 3840 x 2160
+wl = synthetic.binning_workload(10_000_000 if big else 2_000_000, 3840 if big else 1920, 2160 if big else 1080,
+                                seed=0, device="cuda")
 end = 32 + primitives.higher_msb(wl.num_tiles)
 for _ in range(10):
     primitives.sort_pairs(wl.keys, wl.values, 0, end)
@@ -17,8 +19,9 @@ with _lib.kernel_timer() as kt:
         primitives.sort_pairs(wl.keys, wl.values, 0, end)
     torch.cuda.synchronize()
     out = []
-    for nm in ("radix_hist_u64", "radix_digit_scan", "radix_scatter_u64", "segment_ranges", "segment_sort", "scan_reduce", "scan_downsweep"):
+    for nm in ("radix_hist_u64", "radix_digit_scan", "radix_scatter_u64", "segment_ranges", "segment_sort",
+               "big_segments"):
         ms, n = kt.get(nm)
         if n:
             out.append(f"{nm} {ms * 1e3 / n:.1f}us")
-print(os.environ.get("HIDEGS_LIB", "default"), " ".join(out), flush=True)
+print(os.environ.get("HIDEGS_LIB", "default"), "4k" if big else "1080p", " ".join(out), flush=True)
