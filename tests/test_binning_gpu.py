@@ -305,3 +305,51 @@ def test_several_hot_tiles_back_to_back_calls():
         ko, vo, r = primitives.sort_tile_pairs(kd, vd, T)
         assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
         assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+
+
+@pytest.mark.parametrize("case", ["n_multiple_of_tile", "boundary_on_tile_edge", "sparse_low_bits", "empty_tail",
+                                  "one_pass"])
+def test_segment_starts_edge_cases(case):
+    """The last scatter pass writes each segment's first position (csrc/primitives.hip,
+    radix_scatter_kernel<K, true>): the low-bit boundaries it finds per 4096-pair tile -- n a multiple
+    of the tile, a low value starting exactly on a tile edge, most low values absent (several
+    boundaries at one position), trailing absent values (boundary at n), and the one-pass form --
+    must give the oracle's sort and tile ranges."""
+    g = np.random.default_rng(sum(map(ord, case)))
+    T = 8160
+    if case == "n_multiple_of_tile":
+        K = 4096 * 160
+        tiles = g.integers(0, T, K)
+    elif case == "boundary_on_tile_edge":  # low 6 bits: tiles with low value 0 hold exactly 4096 * 20 pairs
+        K = 700_000
+        tiles = g.integers(0, T, K)
+        low0 = (tiles & 63) == 0
+        n0 = int(low0.sum())
+        need = 4096 * 20
+        idx = np.flatnonzero(~low0)[: max(0, need - n0)]
+        tiles[idx] = (tiles[idx] & ~63)  # move pairs into low value 0
+        extra = np.flatnonzero((tiles & 63) == 0)[need:]
+        tiles[extra] = tiles[extra] | 1
+        assert int(((tiles & 63) == 0).sum()) == need
+    elif case == "sparse_low_bits":  # only low values 5 and 40 occur
+        K = 600_000
+        tiles = (g.integers(0, T // 64, K) << 6) | g.choice(np.array([5, 40]), K)
+        tiles = np.minimum(tiles, T - 1)
+    elif case == "empty_tail":  # only tiles < 2000: high digits and low values at the end stay empty
+        K = 600_000
+        tiles = g.integers(0, 2000, K) & ~np.int64(7)
+    else:  # one pass: 200 tiles (8 bits)
+        T = 200
+        K = 300_000
+        tiles = g.integers(0, T, K)
+    depth = g.uniform(0.5, 60.0, K).astype(np.float32).view(np.uint32).astype(np.uint64)
+    keys = (tiles.astype(np.uint64) << np.uint64(32)) | depth
+    vals = np.arange(K, dtype=np.uint32)
+    end = 32 + primitives.higher_msb(T)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, end)
+    ko, vo, r = primitives.sort_tile_pairs(u64(keys), u32(vals), T)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
+    ko2, vo2 = primitives.sort_pairs(u64(keys), u32(vals), 0, end)
+    assert torch.equal(ko2, ko) and torch.equal(vo2, vo)
