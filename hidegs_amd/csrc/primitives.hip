@@ -810,7 +810,10 @@ static_assert(sizeof(BucketShared) >= kSegRun * (sizeof(uint64_t) + sizeof(uint3
 // writing, so no wait is on a workgroup that is not running.  Ordering across workgroups (and XCD
 // L2s) is by agent-scope release / acquire: job payload and pair data before the tag, phase data
 // before `pending`.
-constexpr int kChunk = 2 * kBigStep;  // 4096 pairs per chunk job
+#ifndef HIDEGS_CHUNK_STEPS
+#define HIDEGS_CHUNK_STEPS 2
+#endif
+constexpr int kChunk = HIDEGS_CHUNK_STEPS * kBigStep;  // pairs per chunk job
 #ifndef HIDEGS_QUEUE_BLOCKS
 #define HIDEGS_QUEUE_BLOCKS 256  // queue workers (experiments: tools/build_variant.py)
 #endif
@@ -1041,6 +1044,76 @@ __device__ __forceinline__ void plan_scatter(uint32_t* col, const uint32_t chunk
     col[(chunks + 3) * kRadix] = 0u;
 }
 
+// The last chunk of a record's SCATTER phase (all of its pairs are in buffer dst, and col -- this
+// thread's digit column of the record's pool -- holds the digit starts, totals and AND / OR rows):
+// cut the record into the pieces the queue sorts next, as runs in e (thread 0 publishes them with
+// emit_jobs).  Every thread of the workgroup calls it.
+__device__ __forceinline__ void cut_pieces(const BigQueue& q, EmitShared& e, BigShared& sh, const uint32_t* col,
+                                           const uint32_t chunks, const uint32_t begin, const uint32_t m,
+                                           const int shift, const uint32_t dst)
+{
+    const int t = threadIdx.x;
+    // cut the record into pieces, one thread per digit:
+    //  * a digit of more than kSegCap pairs: a record of the next level (its varying
+    //    bits are known: HIST jobs directly);
+    //  * a digit of more than kSegRun pairs: a SMALL piece of its own;
+    //  * other non-empty digits: SMALL pieces of consecutive digits whose starts share
+    //    a kSegRun-aligned window (so a piece holds < 2 * kSegRun = kSegCap pairs).
+    const uint32_t n_d = col[(chunks + 1) * kRadix];  // 0 above the digit mask
+    const uint32_t s_d = col[chunks * kRadix];        // relative start
+    const uint32_t diff_d = col[(chunks + 2) * kRadix] ^ col[(chunks + 3) * kRadix];
+    if (shift == 0) {  // every varying bit is placed: the record is sorted
+        if (t == 0) {
+            runs_begin(e);
+            if (dst) add_run(e, J_COPY, 1u, begin, m, chunks);
+        }
+    } else {
+        const bool nonempty = n_d != 0u, solo = n_d > (uint32_t)kSegRun;
+        uint32_t* pv = sh.hist;  // previous non-empty digit + 1: inclusive max-scan
+        uint32_t* nx = sh.run;   // start of the next piece: suffix min-scan
+        pv[t] = nonempty ? (uint32_t)t + 1u : 0u;
+        sh.cnt[0][t] = solo;
+        sh.cnt[1][t] = s_d;
+        __syncthreads();
+        for (int o = 1; o < kRadix; o <<= 1) {
+            const uint32_t x = t >= o ? pv[t - o] : 0u;
+            __syncthreads();
+            pv[t] = x > pv[t] ? x : pv[t];
+            __syncthreads();
+        }
+        const uint32_t prev = t ? pv[t - 1] : 0u;
+        const bool boundary = nonempty && (prev == 0u || solo || sh.cnt[0][prev - 1] != 0u ||
+                                           (s_d / kSegRun) != (sh.cnt[1][prev - 1] / kSegRun));
+        nx[t] = boundary ? s_d : m;
+        __syncthreads();
+        for (int o = 1; o < kRadix; o <<= 1) {
+            const uint32_t x = t + o < kRadix ? nx[t + o] : m;
+            __syncthreads();
+            nx[t] = x < nx[t] ? x : nx[t];
+            __syncthreads();
+        }
+        const uint32_t next = t + 1 < kRadix ? nx[t + 1] : m;
+        uint4 run = make_uint4(0u, 0u, 0u, 0u);
+        if (boundary) {
+            if (n_d > (uint32_t)kSegCap)
+                run = record_run(q, begin + s_d, n_d, dst, diff_d);
+            else if (next - s_d > 1u || dst)
+                run = make_uint4(J_SMALL | (dst << 8), begin + s_d, next - s_d, 1u);
+        }
+        uint32_t nruns, total;
+        const uint32_t ri = block_exclusive_scan(run.w ? 1u : 0u, sh.wave, &nruns);
+        const uint32_t ro = block_exclusive_scan(run.w, sh.wave, &total);
+        if (run.w) {
+            e.run[ri] = run;
+            e.off[ri] = ro;
+        }
+        if (t == 0) {
+            e.nruns = nruns;
+            e.off[nruns] = total;
+        }
+    }
+}
+
 union SegLds {
     SegShared lsd;
     BucketShared bucket;
@@ -1048,6 +1121,8 @@ union SegLds {
     struct {
         BigShared big;
         EmitShared emit;
+        uint32_t list[kBlock];  // segment_sort_kernel's scouts: the hot tiles of one sweep
+        uint32_t nlist;
     } queue;
 };
 
@@ -1217,7 +1292,16 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
 #define HIDEGS_OPEN_LOCAL 24576
 #endif
 constexpr int kOpenLocal = HIDEGS_OPEN_LOCAL;
-__device__ __forceinline__ void open_local(const uint64_t* keys, const BigQueue& q, const uint32_t begin,
+#ifndef HIDEGS_SCATTER_LOCAL
+#define HIDEGS_SCATTER_LOCAL 16384  // ... and up to this many, its SCATTER phase too
+#endif
+constexpr int kScatterLocal = HIDEGS_SCATTER_LOCAL;
+#ifndef HIDEGS_SCOUTS
+#define HIDEGS_SCOUTS 16  // segment_sort_kernel's first workgroups, which start the hot tiles (0: own workgroup)
+#endif
+constexpr int kScouts = HIDEGS_SCOUTS;
+__device__ __forceinline__ void open_local(const uint64_t* keys, const uint32_t* vals, const BigQueue& q,
+                                           const uint32_t begin,
                                            const uint32_t m, BigShared& sh, EmitShared& e, uint32_t* s_and,
                                            uint32_t* s_or)
 {
@@ -1270,7 +1354,23 @@ __device__ __forceinline__ void open_local(const uint64_t* keys, const BigQueue&
         }
         __syncthreads();
         plan_scatter(col, chunks, begin, sh);
-        if (t == 0) {
+        if (m <= (uint32_t)kScatterLocal) {
+            // and the SCATTER phase too: only the pieces go to the queue
+            sh.aux[0][t] = 0xffffffffu;
+            sh.aux[1][t] = 0u;
+            for (uint32_t c = 0; c < chunks; c++) {
+                const uint32_t c0 = c * kChunk, cnt = m - c0 < (uint32_t)kChunk ? m - c0 : (uint32_t)kChunk;
+                sh.run[t] = col[c * kRadix];
+                for (uint32_t b = 0; b < cnt; b += kBigStep)
+                    scatter_step<true>(keys, vals, q.alt_k, q.alt_v, begin + c0 + b,
+                                       cnt - b < (uint32_t)kBigStep ? cnt - b : (uint32_t)kBigStep, shift, mask, begin,
+                                       begin + m, sh);
+            }
+            col[(chunks + 2) * kRadix] = sh.aux[0][t];  // this thread's own column: no barrier needed
+            col[(chunks + 3) * kRadix] = sh.aux[1][t];
+            __syncthreads();
+            cut_pieces(q, e, sh, col, chunks, begin, m, shift, 1u);
+        } else if (t == 0) {
             runs_begin(e);
             add_run(e, J_SCATTER, 0u, rec, 0u, chunks);  // pending == chunks already
         }
@@ -1282,14 +1382,44 @@ __device__ __forceinline__ void open_local(const uint64_t* keys, const BigQueue&
 // than kSegCap pairs becomes a record of the partition queue (big_segment_kernel runs it).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_SEG_WAVES))) void segment_sort_kernel(
     uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint32_t* __restrict__ starts,
-    uint2* __restrict__ ranges_out, const BigQueue q)
+    uint2* __restrict__ ranges_out, const int nseg, const BigQueue q)
 {
     __shared__ __attribute__((aligned(16))) SegLds lds;
     __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock], s_max[kWavesPerBlock];
-    // segment b is [starts[b], starts[b + 1]); with ranges_out it is also tile b's range, (0, 0) when
-    // empty -- identifyTileRanges' result
-    const uint2 r = make_uint2(starts[blockIdx.x], starts[blockIdx.x + 1]);
-    if (ranges_out && threadIdx.x == 0) ranges_out[blockIdx.x] = r.y > r.x ? r : make_uint2(0u, 0u);
+    if (kScouts > 0 && blockIdx.x < (unsigned)kScouts) {
+        // a scout: the first workgroups dispatched find the hot tiles (over kQueueMin pairs) and start
+        // them -- the local phases of open_local, or a queue record -- while the other workgroups sort
+        // the ordinary tiles, instead of wherever in the grid the hot tile's own workgroup would run
+        uint32_t* list = lds.queue.list;
+        for (uint32_t s0 = blockIdx.x * kBlock; s0 < (uint32_t)nseg; s0 += kScouts * kBlock) {
+            if (threadIdx.x == 0) lds.queue.nlist = 0u;
+            __syncthreads();
+            const uint32_t sg = s0 + threadIdx.x;
+            if (sg < (uint32_t)nseg && starts[sg + 1] - starts[sg] > (uint32_t)kQueueMin)
+                list[atomicAdd(&lds.queue.nlist, 1u)] = sg;
+            __syncthreads();
+            const uint32_t nl = lds.queue.nlist;  // workgroup-uniform
+            for (uint32_t j = 0; j < nl; j++) {
+                const uint32_t sg2 = list[j], b = starts[sg2], mm = starts[sg2 + 1] - b;
+                if (mm <= (uint32_t)kOpenLocal) {
+                    open_local(keys, vals, q, b, mm, lds.queue.big, lds.queue.emit, s_and, s_or);
+                } else {
+                    if (threadIdx.x == 0) {
+                        runs_begin(lds.queue.emit);
+                        add_run(lds.queue.emit, record_run(q, b, mm, 0u, ~0u));
+                    }
+                    emit_jobs(q, lds.queue.emit);
+                }
+                __syncthreads();  // the LDS is reused by the next one
+            }
+        }
+        return;
+    }
+    const uint32_t seg = blockIdx.x - kScouts;
+    // segment seg is [starts[seg], starts[seg + 1]); with ranges_out it is also tile seg's range,
+    // (0, 0) when empty -- identifyTileRanges' result
+    const uint2 r = make_uint2(starts[seg], starts[seg + 1]);
+    if (ranges_out && threadIdx.x == 0) ranges_out[seg] = r.y > r.x ? r : make_uint2(0u, 0u);
     const uint32_t begin = r.x, m = r.y - r.x;
     if (r.y <= r.x + 1) return;  // absent or single pair: already in place
     if (m > (uint32_t)kSegCap) {
@@ -1297,8 +1427,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
             segment_sort_global(keys, vals, q.alt_k, q.alt_v, begin, m, lds.big);
             return;
         }
+        if (kScouts > 0) return;  // hot: a scout has it
         if (m <= (uint32_t)kOpenLocal) {
-            open_local(keys, q, begin, m, lds.queue.big, lds.queue.emit, s_and, s_or);
+            open_local(keys, vals, q, begin, m, lds.queue.big, lds.queue.emit, s_and, s_or);
             return;
         }
         if (threadIdx.x == 0) {
@@ -1613,65 +1744,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                                           __HIP_MEMORY_SCOPE_AGENT);
                 }
                 if (finish_phase(s, &s_flag)) {
-                    // cut the record into pieces, one thread per digit:
-                    //  * a digit of more than kSegCap pairs: a record of the next level (its varying
-                    //    bits are known: HIST jobs directly);
-                    //  * a digit of more than kSegRun pairs: a SMALL piece of its own;
-                    //  * other non-empty digits: SMALL pieces of consecutive digits whose starts share
-                    //    a kSegRun-aligned window (so a piece holds < 2 * kSegRun = kSegCap pairs).
-                    const uint32_t n_d = col[(chunks + 1) * kRadix];  // 0 above the digit mask
-                    const uint32_t s_d = col[chunks * kRadix];        // relative start
-                    const uint32_t diff_d = col[(chunks + 2) * kRadix] ^ col[(chunks + 3) * kRadix];
-                    if (shift == 0) {  // every varying bit is placed: the record is sorted
-                        if (t == 0) {
-                            runs_begin(e);
-                            if (dst) add_run(e, J_COPY, 1u, begin, m, chunks);
-                        }
-                    } else {
-                        const bool nonempty = n_d != 0u, solo = n_d > (uint32_t)kSegRun;
-                        uint32_t* pv = sh.hist;  // previous non-empty digit + 1: inclusive max-scan
-                        uint32_t* nx = sh.run;   // start of the next piece: suffix min-scan
-                        pv[t] = nonempty ? (uint32_t)t + 1u : 0u;
-                        sh.cnt[0][t] = solo;
-                        sh.cnt[1][t] = s_d;
-                        __syncthreads();
-                        for (int o = 1; o < kRadix; o <<= 1) {
-                            const uint32_t x = t >= o ? pv[t - o] : 0u;
-                            __syncthreads();
-                            pv[t] = x > pv[t] ? x : pv[t];
-                            __syncthreads();
-                        }
-                        const uint32_t prev = t ? pv[t - 1] : 0u;
-                        const bool boundary = nonempty && (prev == 0u || solo || sh.cnt[0][prev - 1] != 0u ||
-                                                           (s_d / kSegRun) != (sh.cnt[1][prev - 1] / kSegRun));
-                        nx[t] = boundary ? s_d : m;
-                        __syncthreads();
-                        for (int o = 1; o < kRadix; o <<= 1) {
-                            const uint32_t x = t + o < kRadix ? nx[t + o] : m;
-                            __syncthreads();
-                            nx[t] = x < nx[t] ? x : nx[t];
-                            __syncthreads();
-                        }
-                        const uint32_t next = t + 1 < kRadix ? nx[t + 1] : m;
-                        uint4 run = make_uint4(0u, 0u, 0u, 0u);
-                        if (boundary) {
-                            if (n_d > (uint32_t)kSegCap)
-                                run = record_run(q, begin + s_d, n_d, dst, diff_d);
-                            else if (next - s_d > 1u || dst)
-                                run = make_uint4(J_SMALL | (dst << 8), begin + s_d, next - s_d, 1u);
-                        }
-                        uint32_t nruns, total;
-                        const uint32_t ri = block_exclusive_scan(run.w ? 1u : 0u, sh.wave, &nruns);
-                        const uint32_t ro = block_exclusive_scan(run.w, sh.wave, &total);
-                        if (run.w) {
-                            e.run[ri] = run;
-                            e.off[ri] = ro;
-                        }
-                        if (t == 0) {
-                            e.nruns = nruns;
-                            e.off[nruns] = total;
-                        }
-                    }
+                    cut_pieces(q, e, sh, col, chunks, begin, m, shift, dst);
                     emit_jobs(q, e);
                 }
             }
@@ -1897,8 +1970,8 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
     }
     if (segmented) {
         uint64_t* ko = reinterpret_cast<uint64_t*>(keys_out);
-        HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg), dim3(kBlock), 0, stream, ko, vals_out,
-                      seg_starts, ranges_out, q);
+        HIDEGS_LAUNCH("segment_sort", segment_sort_kernel, dim3(nseg + kScouts), dim3(kBlock), 0, stream, ko,
+                      vals_out, seg_starts, ranges_out, nseg, q);
         HIDEGS_LAUNCH("big_segments", big_segment_kernel, dim3(kQueueBlocks), dim3(kBlock), 0, stream, ko, vals_out,
                       reinterpret_cast<uint64_t*>(alt_k), alt_v, q);
     } else if (ranges_out) {
