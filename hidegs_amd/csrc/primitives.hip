@@ -818,6 +818,9 @@ constexpr int kChunk = HIDEGS_CHUNK_STEPS * kBigStep;  // pairs per chunk job
 #define HIDEGS_QUEUE_BLOCKS 256  // queue workers (experiments: tools/build_variant.py)
 #endif
 constexpr int kQueueBlocks = HIDEGS_QUEUE_BLOCKS;
+#ifndef HIDEGS_BACKOFF_MAX
+#define HIDEGS_BACKOFF_MAX 16  // a waiting worker's longest sleep between polls, in s_sleep(8) units
+#endif
 #ifndef HIDEGS_QUEUE_MIN
 #define HIDEGS_QUEUE_MIN 8192  // segments up to this many pairs: the one-workgroup global form
 #endif
@@ -1632,7 +1635,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                     if (d == r && i >= r) break;  // nothing queued, nothing in flight: the end
                 }
                 for (uint32_t k = 0; k < backoff; k++) __builtin_amdgcn_s_sleep(8);  // ~0.2 us each
-                backoff = backoff < 16u ? 2u * backoff : 16u;
+                backoff = backoff < (uint32_t)HIDEGS_BACKOFF_MAX ? 2u * backoff : (uint32_t)HIDEGS_BACKOFF_MAX;
             }
             if (polls == kMaxPolls) q_flag(q, 4u);
             s_job = job;
