@@ -45,22 +45,27 @@ constexpr int kRadix = 1 << kRadixBits;     // 256
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // ============================== scan ===========================================
+#ifndef HIDEGS_SCAN_ITEMS
+#define HIDEGS_SCAN_ITEMS 16  // u32 items per thread of a scan tile (experiments: tools/build_variant.py)
+#endif
+constexpr int kDevScanItems = HIDEGS_SCAN_ITEMS;
+constexpr int kDevScanTile = kBlock * kDevScanItems;
 
 // Loads one tile of u32 (striped 16-byte loads) and leaves it in LDS.
 __device__ __forceinline__ void load_tile_u32(const uint32_t* in, long long base, long long n,
                                               uint32_t* s_tile)
 {
     const int t = threadIdx.x;
-    if (base + kTile <= n && ((reinterpret_cast<uintptr_t>(in) & 15) == 0)) {
+    if (base + kDevScanTile <= n && ((reinterpret_cast<uintptr_t>(in) & 15) == 0)) {
         const uint4* src = reinterpret_cast<const uint4*>(in + base);
 #pragma unroll
-        for (int j = 0; j < kItems / 4; j++) {
+        for (int j = 0; j < kDevScanItems / 4; j++) {
             uint4 v = src[j * kBlock + t];
             reinterpret_cast<uint4*>(s_tile)[j * kBlock + t] = v;
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < kItems; j++) {
+        for (int j = 0; j < kDevScanItems; j++) {
             long long i = base + j * kBlock + t;
             s_tile[j * kBlock + t] = (i < n) ? in[i] : 0u;
         }
@@ -71,13 +76,13 @@ __device__ __forceinline__ void load_tile_u32(const uint32_t* in, long long base
 __global__ __launch_bounds__(kBlock) void scan_reduce_kernel(const uint32_t* __restrict__ in, long long n,
                                                              uint32_t* __restrict__ tile_sums)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_tile[kTile];
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[kDevScanTile];
     __shared__ uint32_t s_wave[kWavesPerBlock];
-    const long long base = (long long)blockIdx.x * kTile;
+    const long long base = (long long)blockIdx.x * kDevScanTile;
     load_tile_u32(in, base, n, s_tile);
     uint32_t sum = 0;
 #pragma unroll
-    for (int j = 0; j < kItems; j++) sum += s_tile[threadIdx.x * kItems + j];
+    for (int j = 0; j < kDevScanItems; j++) sum += s_tile[threadIdx.x * kDevScanItems + j];
     uint32_t total;
     block_exclusive_scan(sum, s_wave, &total);
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
@@ -92,9 +97,9 @@ __global__ __launch_bounds__(kBlock) void scan_downsweep_kernel(const uint32_t* 
                                                                 const uint32_t* __restrict__ tile_offsets,
                                                                 int sums_raw, uint32_t* out)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_tile[kTile];
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[kDevScanTile];
     __shared__ uint32_t s_wave[kWavesPerBlock];
-    const long long base = (long long)blockIdx.x * kTile;
+    const long long base = (long long)blockIdx.x * kDevScanTile;
     uint32_t tile_off;
     if (sums_raw) {
         uint32_t part = 0;
@@ -104,28 +109,28 @@ __global__ __launch_bounds__(kBlock) void scan_downsweep_kernel(const uint32_t* 
         tile_off = tile_offsets[blockIdx.x];
     }
     load_tile_u32(in, base, n, s_tile);
-    uint32_t v[kItems];
+    uint32_t v[kDevScanItems];
     uint32_t sum = 0;
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
-        v[j] = s_tile[threadIdx.x * kItems + j];
+    for (int j = 0; j < kDevScanItems; j++) {
+        v[j] = s_tile[threadIdx.x * kDevScanItems + j];
         sum += v[j];
     }
     uint32_t total;
     uint32_t run = block_exclusive_scan(sum, s_wave, &total) + tile_off;
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < kDevScanItems; j++) {
         run += v[j];
-        s_tile[threadIdx.x * kItems + j] = run;  // inclusive
+        s_tile[threadIdx.x * kDevScanItems + j] = run;  // inclusive
     }
     __syncthreads();
-    if (base + kTile <= n && ((reinterpret_cast<uintptr_t>(out) & 15) == 0)) {
+    if (base + kDevScanTile <= n && ((reinterpret_cast<uintptr_t>(out) & 15) == 0)) {
         uint4* dst = reinterpret_cast<uint4*>(out + base);
 #pragma unroll
-        for (int j = 0; j < kItems / 4; j++) dst[j * kBlock + threadIdx.x] = reinterpret_cast<uint4*>(s_tile)[j * kBlock + threadIdx.x];
+        for (int j = 0; j < kDevScanItems / 4; j++) dst[j * kBlock + threadIdx.x] = reinterpret_cast<uint4*>(s_tile)[j * kBlock + threadIdx.x];
     } else {
 #pragma unroll
-        for (int j = 0; j < kItems; j++) {
+        for (int j = 0; j < kDevScanItems; j++) {
             long long i = base + j * kBlock + threadIdx.x;
             if (i < n) out[i] = s_tile[j * kBlock + threadIdx.x];
         }
@@ -1825,7 +1830,7 @@ __global__ __launch_bounds__(kBlock) void identify_ranges_kernel(const uint64_t*
 
 size_t scan_scratch(long long n)
 {
-    const int nt = ceil_div(n, kTile);
+    const int nt = ceil_div(n, kDevScanTile);
     return align_up((size_t)nt * sizeof(uint32_t)) + align_up(sizeof(uint32_t));
 }
 
@@ -1994,7 +1999,7 @@ int inclusive_scan_u32(void* scratch, size_t scratch_bytes, const uint32_t* in, 
     if (n == 0) return 0;
     if (!in || !out) return fail(HIDEGS_E_ARG, "inclusive_scan_u32: NULL pointer");
     if (!scratch || scratch_bytes < scan_scratch(n)) return fail(HIDEGS_E_ARG, "inclusive_scan_u32: scratch too small");
-    const int nt = ceil_div(n, kTile);
+    const int nt = ceil_div(n, kDevScanTile);
     Carver c(scratch);
     uint32_t* sums = c.take<uint32_t>(nt);
     HIDEGS_LAUNCH("scan_reduce", scan_reduce_kernel, dim3(nt), dim3(kBlock), 0, stream, in, n, sums);
