@@ -63,6 +63,8 @@ SIGNATURES = {
     "hidegs_sort_pairs_u32": (I, [P, SZ, P, P, P, P, LL, I, I, P]),
     "hidegs_identify_tile_ranges": (I, [P, LL, P, I, P]),
     "hidegs_sort_tile_pairs": (I, [P, SZ, P, P, P, P, LL, I, P, P]),
+    "hidegs_queue_error": (I, [P, I, P]),
+    "hidegs_set_debug": (None, [I]),
     "hidegs_higher_msb": (U32, [U32]),
     "hidegs_masked_adam": (I, [P, P, P, P, P, LL, I, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                                 LL, P]),
@@ -78,6 +80,20 @@ _lib = None
 _lock = threading.Lock()
 
 
+def load_library(path: str) -> C.CDLL:
+    """A build of the ABI at `path` with every signature of include/hidegs.h bound (lib() for the
+    product build; tests load the build.VARIANTS this way)."""
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: run `python -m hidegs_amd.build` "
+                           "(or __graft_entry__.build()) to compile it for gfx950")
+    dll = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(dll, name)
+        fn.restype = res
+        fn.argtypes = args
+    return dll
+
+
 def lib() -> C.CDLL:
     """Load libhidegs.so once; raise RuntimeError if it was not built."""
     global _lib
@@ -85,15 +101,7 @@ def lib() -> C.CDLL:
         return _lib
     with _lock:
         if _lib is None:
-            if not os.path.exists(LIB_PATH):
-                raise RuntimeError(f"{LIB_PATH} is missing: run `python -m hidegs_amd.build` "
-                                   "(or __graft_entry__.build()) to compile it for gfx950")
-            dll = C.CDLL(LIB_PATH)
-            for name, (res, args) in SIGNATURES.items():
-                fn = getattr(dll, name)
-                fn.restype = res
-                fn.argtypes = args
-            _lib = dll
+            _lib = load_library(LIB_PATH)
     return _lib
 
 

@@ -6,10 +6,13 @@
 // They fail loudly with HIDEGS_E_UNSUPPORTED; nothing falls back to a CPU path.
 #include "common.h"
 
+#include <atomic>
+
 namespace hidegs {
 
 namespace {
 thread_local std::string g_last_error;
+std::atomic<int> g_debug{0};
 constexpr const char* kNotBuilt =
     "not built: the gfx950 rasterizer kernels are outside this release (DESIGN.md, 'Decisions in force')";
 }  // namespace
@@ -17,10 +20,12 @@ constexpr const char* kNotBuilt =
 void set_error(const std::string& msg) { g_last_error = msg; }
 const std::string& last_error() { return g_last_error; }
 
+bool debug_enabled() { return g_debug.load(std::memory_order_relaxed) != 0; }
+
 int check_launch(const char* stage, hipStream_t stream, int debug)
 {
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && debug) e = hipStreamSynchronize(stream);
+    if (e == hipSuccess && (debug || debug_enabled())) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return fail(HIDEGS_E_HIP, std::string(stage) + ": " + hipGetErrorString(e));
     return 0;
 }
@@ -55,6 +60,8 @@ int hidegs_mark_visible(int, const float*, const float*, const float*, unsigned 
 {
     return hidegs::not_built("hidegs_mark_visible");
 }
+
+void hidegs_set_debug(int enable) { hidegs::g_debug.store(enable ? 1 : 0, std::memory_order_relaxed); }
 
 const char* hidegs_last_error(void) { return hidegs::last_error().c_str(); }
 const char* hidegs_version(void) { return "hidegs-abi 0.4 (gfx950: distCUDA2, scan, radix sort, tile sort + ranges, masked Adam)"; }

@@ -28,6 +28,13 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // (the reference's CHECK_CUDA(..., debug), auxiliary.h:23-30).
 int check_launch(const char* stage, hipStream_t stream, int debug);
 
+// Library-wide debug mode (hidegs_set_debug): every launch check synchronises, and the sort reads
+// back the partition queue's error word.
+bool debug_enabled();
+
+// Sticky partition-queue error word of the current device (primitives.hip); synchronises `stream`.
+int queue_error(hipStream_t stream, int clear, uint32_t* flags);
+
 // 256-byte aligned carving of one caller-provided scratch buffer.
 constexpr size_t kAlign = 256;
 inline size_t align_up(size_t n) { return (n + kAlign - 1) & ~(kAlign - 1); }

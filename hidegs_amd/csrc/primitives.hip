@@ -875,9 +875,14 @@ __device__ __forceinline__ void fence_release() { __builtin_amdgcn_fence(__ATOMI
 // tile ran 1.2 ms): each wave only waits for its own stores to be acknowledged, then after a barrier
 // ONE thread's agent-scope release (L2 writeback) or acquire (invalidate) acts for the workgroup.
 __device__ __forceinline__ void wave_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Sticky per-device copy of every queue error (bit 1: job slots exhausted, bit 4: a worker gave up
+// waiting), read and cleared by hidegs_queue_error(); the debug mode (hidegs_set_debug) checks it after
+// every sort.  A set bit means the sort's output is not trustworthy.
+__device__ uint32_t g_queue_error;
 __device__ __forceinline__ void q_flag(const BigQueue& q, uint32_t bit)
 {
     __hip_atomic_fetch_or(&q.ctl[kCtlStride * Q_ERROR], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_or(&g_queue_error, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Jobs a workgroup is about to enqueue, as runs: `count` jobs of one kind.
@@ -1851,7 +1856,11 @@ BigQueue queue_caps(long long n)
 {
     BigQueue q{};
     q.rec_cap = (uint32_t)(5 * (n / (kSegCap + 1)) + 8);
+#ifdef HIDEGS_JOB_CAP  // tests only: a tiny job capacity forces the overflow path (tests/test_binning_gpu.py)
+    q.job_cap = (uint32_t)HIDEGS_JOB_CAP;
+#else
     q.job_cap = (uint32_t)(n / 24 + 1024);
+#endif
     q.pool_cap = (uint32_t)(n / 2 + 16 * kRadix);
     return q;
 }
@@ -1982,6 +1991,16 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
                       vals_out, seg_starts, ranges_out, nseg, q);
         HIDEGS_LAUNCH("big_segments", big_segment_kernel, dim3(kQueueBlocks), dim3(kBlock), 0, stream, ko, vals_out,
                       reinterpret_cast<uint64_t*>(alt_k), alt_v, q);
+        if (debug_enabled()) {  // debug mode: the queue's own error word, after the grid has drained
+            if (int rc = check_launch(what, stream, 1)) return rc;
+            uint32_t err = 0;
+            if (int rc = queue_error(stream, 1, &err)) return rc;
+            if (err)
+                return fail(HIDEGS_E_HIP, std::string(what) + ": hot-tile partition queue error " + std::to_string(err) +
+                                              ((err & 1u) ? " (job slots exhausted)" : "") +
+                                              ((err & 4u) ? " (a worker gave up waiting)" : "") +
+                                              ": the output is not sorted");
+        }
     } else if (ranges_out) {
         if (int rc = check_launch(what, stream, 0)) return rc;
         return identify_tile_ranges(reinterpret_cast<const uint64_t*>(keys_out), n,
@@ -1991,6 +2010,21 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
 }
 
 }  // namespace
+
+int queue_error(hipStream_t stream, int clear, uint32_t* flags)
+{
+    uint32_t v = 0;
+    if (hipStreamSynchronize(stream) != hipSuccess ||
+        hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_queue_error), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(HIDEGS_E_HIP, "queue_error: readback failed");
+    if (clear && v) {
+        const uint32_t z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_queue_error), &z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
+            return fail(HIDEGS_E_HIP, "queue_error: clear failed");
+    }
+    *flags = v;
+    return 0;
+}
 
 int inclusive_scan_u32(void* scratch, size_t scratch_bytes, const uint32_t* in, uint32_t* out, long long n,
                        hipStream_t stream)
@@ -2091,6 +2125,12 @@ int hidegs_identify_tile_ranges(const uint64_t* sorted_keys, long long n, uint32
                                 void* stream)
 {
     return hidegs::identify_tile_ranges(sorted_keys, n, ranges, num_tiles, hidegs::as_stream(stream));
+}
+
+int hidegs_queue_error(void* stream, int clear, uint32_t* flags)
+{
+    if (!flags) return hidegs::fail(HIDEGS_E_ARG, "hidegs_queue_error: NULL flags");
+    return hidegs::queue_error(hidegs::as_stream(stream), clear, flags);
 }
 
 uint32_t hidegs_higher_msb(uint32_t n)

@@ -59,6 +59,19 @@ class AdamStepPlan:
             with torch.cuda.device(dev):
                 _lib.check(L.hidegs_masked_adam_multi(arr, len(descs), _lib.stream_handle(dev)), "masked Adam")
 
+    def run_except(self, params) -> None:
+        """The update of every parameter of the plan not in `params` (whole), as run() would."""
+        skip = {id(p) for p in params}
+        batches = {}
+        for p, dev, desc, _ in self._entries:
+            if id(p) not in skip:
+                batches.setdefault(dev, []).append(desc)
+        L = _lib.lib()
+        for dev, descs in batches.items():
+            arr = (_lib.AdamTensor * len(descs))(*descs)
+            with torch.cuda.device(dev):
+                _lib.check(L.hidegs_masked_adam_multi(arr, len(descs), _lib.stream_handle(dev)), "masked Adam")
+
     def run_rows(self, param, row_start: int, row_end: int) -> None:
         i = self._index.get(id(param))
         if i is None:

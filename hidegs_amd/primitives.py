@@ -119,3 +119,21 @@ def identify_tile_ranges(sorted_keys: torch.Tensor, num_tiles: int) -> torch.Ten
                                                     _lib.stream_handle(dev))
         _lib.check(rc, "identify_tile_ranges")
     return ranges
+
+
+def queue_error(device=None, clear: bool = True) -> int:
+    """Sticky error word of the hot-tile partition queue on `device` (hidegs_queue_error): 0, or
+    bit 1 (job slots exhausted) / bit 4 (a worker gave up) if some sort since the last clear returned
+    pairs that are not fully sorted.  Synchronises the current stream."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    flags = _lib.C.c_uint32(0)
+    with torch.cuda.device(dev):
+        rc = _lib.lib().hidegs_queue_error(_lib.stream_handle(dev), int(bool(clear)), _lib.C.byref(flags))
+    _lib.check(rc, "queue_error")
+    return int(flags.value)
+
+
+def set_debug(enable: bool) -> None:
+    """Library-wide debug mode (hidegs_set_debug): synchronising launch checks, and every sort
+    verifies the partition queue's error word and raises RuntimeError if it is set."""
+    _lib.lib().hidegs_set_debug(int(bool(enable)))

@@ -76,6 +76,12 @@ class GradArena:
 
     `views[name]` is a contiguous (n, width) view; `attach` makes it the `.grad` of a
     parameter (autograd then accumulates into it in place, shape-matched via view_as).
+
+    The link is the parameter's `.grad` object itself: `optimizer.zero_grad(set_to_none=True)`
+    (the 3DGS default), re-creating the parameters (densification) or assigning `.grad` detaches
+    it, and autograd then writes a fresh tensor the arena never sees.  Call `zero_()` instead of
+    zero_grad, and `attach` again after the parameters change; the exchange checks the link
+    (`check_attached`) and raises when it is broken.
     """
 
     def __init__(self, n: int, widths: Dict[str, int] = None, device=None, dtype=torch.float32):
@@ -95,6 +101,19 @@ class GradArena:
             if p.numel() != v.numel():
                 raise ValueError(f"{name}: parameter has {p.numel()} values, arena slot {v.numel()}")
             p.grad = v.view_as(p)
+
+    def check_attached(self, params: Dict[str, torch.Tensor]) -> None:
+        """Raise if some params[name].grad is not this arena's view (the gradient would be summed
+        from stale arena rows while the optimizer stepped the local one: replicas drift apart)."""
+        for name, p in params.items():
+            if name not in self.views:
+                continue
+            g = p.grad
+            v = self.views[name]
+            if g is None or g.data_ptr() != v.data_ptr() or g.numel() != v.numel():
+                raise RuntimeError(f"view-DP: {name}.grad is not the gradient arena's view (zero_grad(set_to_none="
+                                   "True), re-created parameters or a reassigned .grad detach it); call "
+                                   "arena.attach(params) again and clear gradients with arena.zero_()")
 
     def zero_(self) -> None:
         self.flat.zero_()
@@ -245,10 +264,13 @@ class ViewDPExchange:
 
     # ---- the whole exchange step ----------------------------------------------------
     def exchange(self, grads: Union[GradArena, Dict[str, torch.Tensor]], visible: torch.Tensor,
-                 max_stats: Optional[List[torch.Tensor]] = None) -> ExchangeResult:
+                 max_stats: Optional[List[torch.Tensor]] = None,
+                 params: Optional[Dict[str, torch.Tensor]] = None) -> ExchangeResult:
         """Run one exchange step.
 
         grads      GradArena or {name: (N, w) grad}; summed in place.
+        params     with a GradArena: the parameters attached to it; their `.grad` must still be
+                   the arena's views (checked: RuntimeError otherwise).
         visible    this rank's visibility filter (radii > 0), bool (N,).
         max_stats  this step's per-Gaussian maxima (e.g. the view-space gradient norm of
                    visible rows, radii), reduced in place by MAX.
@@ -257,6 +279,8 @@ class ViewDPExchange:
             xyz_gradient_accum = max(xyz_gradient_accum, norm)   # on union rows
             denom += view_count
         """
+        if params is not None and isinstance(grads, GradArena):
+            grads.check_attached(params)
         self.last = ExchangeStats()
         union, count = self.gather_visibility(visible)
         g = grads if isinstance(grads, GradArena) else grads.values()
@@ -285,15 +309,15 @@ class ViewDPExchange:
         missing = [k for k in arena.widths if k not in params]
         if missing:
             raise KeyError(f"no parameter for arena fields {missing}")
+        arena.check_attached(params)
         self.last = ExchangeStats()
         union, count = self.gather_visibility(visible)
-        plan = optimizer.begin_step(union)
         n = arena.n
         world = dist.get_world_size(self.group)
         nu = int(union.sum()) if n else 0
         if world == 1 or n == 0 or nu < self.compact_below * n:
             self.sum_gradients(arena, union)
-            plan.run()
+            optimizer.begin_step(union).run()  # counters advance only once the gradients are summed
         else:
             self.last.union_rows = nu
             works = []
@@ -306,8 +330,13 @@ class ViewDPExchange:
                                                   async_op=True), name, r0, r1))
             self.last.collectives += len(works)
             self.last.reduced_bytes += arena.flat.numel() * arena.flat.element_size()
+            # the step counters advance once every collective has been issued
+            plan = optimizer.begin_step(union)
             for work, name, r0, r1 in works:
                 work.wait()  # the current stream waits for this bucket; later buckets keep reducing
                 plan.run_rows(params[name], r0, r1)
+            # parameters the plan steps that are not arena fields (their gradients were not exchanged
+            # here): stepped whole, as optimizer.step(union) would
+            plan.run_except([params[k] for k in arena.widths])
         self.max_stats(max_stats or [])
         return ExchangeResult(union, count)

@@ -152,6 +152,22 @@ int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* 
                            const uint32_t* vals_in, uint32_t* vals_out, long long n, int num_tiles, uint32_t* ranges,
                            void* stream);
 
+/*
+ * [host] Error word of the hot-tile partition queue inside hidegs_sort_pairs_u64 /
+ * hidegs_sort_tile_pairs, sticky per device since it was last cleared: bit 1 = job slots
+ * exhausted, bit 4 = a queue worker gave up waiting.  Non-zero means some sort since the last
+ * clear returned pairs that are not fully sorted.  Synchronises `stream`; clear != 0 resets it.
+ * In debug mode (hidegs_set_debug) every such sort checks it itself and returns HIDEGS_E_HIP.
+ */
+int hidegs_queue_error(void* stream, int clear, uint32_t* flags);
+
+/*
+ * [host] Library-wide debug mode, the reference's per-call `debug` flag (auxiliary.h:23-30) for
+ * the entry points that have none: every launch check synchronises its stream and reports an
+ * asynchronous fault at its stage, and sorts verify the partition queue's error word.
+ */
+void hidegs_set_debug(int enable);
+
 /* [host] getHigherMsb: bits needed to hold n, at least 1; the sort end bit is 32 + this of the tile count. */
 uint32_t hidegs_higher_msb(uint32_t n);
 

@@ -10,6 +10,14 @@ from oracle import binning
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def queue_clean():
+    """Every sort of every test leaves the partition queue's sticky error word clear."""
+    primitives.queue_error(clear=True)
+    yield
+    assert primitives.queue_error(clear=True) == 0, "a sort in this test reported a partition-queue error"
+
+
 def u64(a):
     return torch.from_numpy(a.view(np.int64)).cuda()
 
@@ -353,3 +361,67 @@ def test_segment_starts_edge_cases(case):
     assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
     ko2, vo2 = primitives.sort_pairs(u64(keys), u32(vals), 0, end)
     assert torch.equal(ko2, ko) and torch.equal(vo2, vo)
+
+
+def test_queue_overflow_is_reported_not_silent():
+    """A build whose partition queue holds 64 job slots (build.VARIANTS['qcap']) cannot queue a 300K-pair
+    hot tile's jobs: the sort must report it -- through the sticky error word (hidegs_queue_error),
+    and in debug mode as the call's own HIDEGS_E_HIP -- rather than return a mis-sorted tile silently.
+    The product build sorts the same input correctly with the word clear."""
+    import ctypes as C
+
+    from hidegs_amd import _lib, build
+    var = _lib.load_library(build.variant_path("qcap"))
+    g = np.random.default_rng(11)
+    T = 1024
+    keys, _ = raster_like_keys(200_000, T, 3)
+    hot = (np.uint64(500) << np.uint64(32)) | g.uniform(0.5, 60.0, 300_000).astype(np.float32).view(
+        np.uint32).astype(np.uint64)
+    keys = np.concatenate([keys, hot])[g.permutation(500_000)]
+    vals = np.arange(keys.size, dtype=np.uint32)
+    kd, vd = u64(keys), u32(vals)
+    n = keys.size
+    dev = kd.device
+    stream = _lib.stream_handle(dev)
+
+    def run():
+        ko, vo = torch.empty_like(kd), torch.empty_like(vd)
+        rng = torch.empty((T, 2), dtype=torch.int32, device=dev)
+        tmp = torch.empty(int(var.hidegs_sort_pairs_u64_scratch_bytes(n)), dtype=torch.uint8, device=dev)
+        rc = var.hidegs_sort_tile_pairs(_lib.ptr(tmp), tmp.numel(), _lib.ptr(kd), _lib.ptr(ko), _lib.ptr(vd),
+                                        _lib.ptr(vo), n, T, _lib.ptr(rng), stream)
+        return rc, vo
+
+    flags = C.c_uint32(0)
+    assert var.hidegs_queue_error(stream, 1, C.byref(flags)) == 0
+    rc, _ = run()
+    assert rc == 0  # without debug mode the call itself cannot know (no host sync) ...
+    assert var.hidegs_queue_error(stream, 1, C.byref(flags)) == 0
+    assert flags.value & 1, "job-slot overflow not reported"  # ... but the sticky word does
+    var.hidegs_set_debug(1)
+    try:
+        rc, _ = run()
+        assert rc == _lib.E_HIP
+        assert b"job slots exhausted" in var.hidegs_last_error()
+    finally:
+        var.hidegs_set_debug(0)
+    assert var.hidegs_queue_error(stream, 1, C.byref(flags)) == 0 and flags.value & 1
+    # the product build: same input, sorted correctly, word clear (checked by the fixture too)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
+    _, vo, _ = primitives.sort_tile_pairs(kd, vd, T)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+
+
+def test_debug_mode_passes_clean_sorts():
+    """Debug mode on the product build: synchronising checks and the queue check, no false alarm."""
+    g = np.random.default_rng(12)
+    T = 1024
+    keys, vals = raster_like_keys(300_000, T, 4)
+    keys[:50_000] = (np.uint64(7) << np.uint64(32)) | (keys[:50_000] & np.uint64(0xFFFFFFFF))  # a hot tile
+    primitives.set_debug(True)
+    try:
+        ko, vo, r = primitives.sort_tile_pairs(u64(keys), u32(vals), T)
+    finally:
+        primitives.set_debug(False)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)

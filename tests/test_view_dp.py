@@ -189,6 +189,9 @@ class RecordingPlan:
         self.calls.append((name, r0, r1))
         self.snap[(name, r0, r1)] = self.arena[name][r0:r1].clone()
 
+    def run_except(self, params):
+        self.rest_skipped = {self.names[id(p)] for p in params}
+
 
 class RecordingOptimizer:
     def __init__(self, plan):
@@ -207,6 +210,7 @@ def worker_step(rank, world, port, compact_below, bucket_bytes, q):
         visible, grads, norm, _ = rank_inputs(rank, 0)
         arena = GradArena(N)
         params = {k: torch.nn.Parameter(torch.zeros(N, w)) for k, w in LEAF_WIDTHS.items()}
+        arena.attach(params)
         for k, v in grads.items():
             arena[k].copy_(v)
         plan = RecordingPlan(arena, {id(p): k for k, p in params.items()})
@@ -233,6 +237,8 @@ def worker_step(rank, world, port, compact_below, bucket_bytes, q):
                                                              key=list(LEAF_WIDTHS).index)
             for (name, r0, r1), got in plan.snap.items():
                 ok = ok and torch.allclose(got, exp[name][r0:r1], atol=1e-5)
+            # the plan's other parameters are stepped whole, the arena fields are skipped there
+            ok = ok and getattr(plan, "rest_skipped", None) == set(LEAF_WIDTHS)
         if rank == 0:
             q.put((ok, mode, ex.last.collectives))
     finally:
@@ -264,3 +270,20 @@ def test_exchange_and_step_steps_each_row_once_after_its_reduction(world, compac
     assert ok and got_mode == mode
     if world == 1:
         assert collectives == 0
+
+
+def test_detached_grad_is_refused():
+    """zero_grad(set_to_none=True) or a reassigned .grad breaks the parameter/arena link: the
+    exchange must raise instead of summing stale arena rows."""
+    arena = GradArena(8)
+    params = {k: torch.nn.Parameter(torch.zeros(8, w)) for k, w in LEAF_WIDTHS.items()}
+    arena.attach(params)
+    arena.check_attached(params)
+    opt = torch.optim.SGD(list(params.values()), lr=0.1)
+    opt.zero_grad(set_to_none=True)
+    with pytest.raises(RuntimeError, match="not the gradient arena's view"):
+        arena.check_attached(params)
+    arena.attach(params)
+    params["xyz"].grad = torch.zeros(8, 3)
+    with pytest.raises(RuntimeError, match="xyz.grad"):
+        ViewDPExchange().exchange(arena, torch.ones(8, dtype=torch.bool), params=params)
