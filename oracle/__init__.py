@@ -8,6 +8,8 @@ simple_knn, hidegs_amd) never import it.
   masked_adam                   -- one OurAdam step on one parameter tensor (adam_ref.c)
   stable_sort_pairs / inclusive_scan_u32 / tile_ranges -- generic integer restatements
      of the binning primitives (numpy), see binning.py
+  sort_pairs_omp                -- the same stable sort as a multi-threaded C radix sort
+                                   (sort_ref.c): the binning step's CPU baseline on all cores
 """
 from __future__ import annotations
 
@@ -40,6 +42,12 @@ def lib() -> C.CDLL:
         dll.oracle_masked_adam.argtypes = [C.c_void_p] * 5 + [C.c_longlong, C.c_int] + [C.c_double] * 5 + \
             [C.c_longlong]
         dll.oracle_masked_adam.restype = None
+        dll.oracle_sort_pairs_u64.argtypes = [C.c_void_p] * 4 + [C.c_longlong, C.c_int, C.c_int, C.c_int]
+        dll.oracle_sort_pairs_u64.restype = C.c_int
+        dll.oracle_set_threads.argtypes = [C.c_int]
+        dll.oracle_set_threads.restype = None
+        dll.oracle_max_threads.argtypes = []
+        dll.oracle_max_threads.restype = C.c_int
         _lib = dll
     return _lib
 
@@ -76,3 +84,23 @@ def masked_adam(param, grad, exp_avg, exp_avg_sq, relevant, lr, beta1=0.9, beta2
     lib().oracle_masked_adam(param.ctypes.data, grad.ctypes.data, exp_avg.ctypes.data, exp_avg_sq.ctypes.data,
                              None if rel is None else rel.ctypes.data, rows, width, lr, beta1, beta2, eps,
                              weight_decay, int(step))
+
+
+def sort_pairs_omp(keys: np.ndarray, vals: np.ndarray, begin_bit: int, end_bit: int, threads: int = 0):
+    """Stable sort of (uint64 key, uint32 value) pairs by key bits [begin_bit, end_bit), OpenMP radix
+    sort on `threads` threads (0: OpenMP's default).  Same result as binning.stable_sort_pairs."""
+    k = np.ascontiguousarray(keys, dtype=np.uint64)
+    v = np.ascontiguousarray(vals, dtype=np.uint32)
+    ko, vo = np.empty_like(k), np.empty_like(v)
+    if k.shape[0]:
+        rc = lib().oracle_sort_pairs_u64(k.ctypes.data, v.ctypes.data, ko.ctypes.data, vo.ctypes.data, k.shape[0],
+                                         int(begin_bit), int(end_bit), int(threads))
+        if rc != 0:
+            raise MemoryError("oracle_sort_pairs_u64: allocation failed")
+    return ko, vo
+
+
+def set_threads(threads: int) -> int:
+    """OpenMP thread count of the oracle's later calls; returns the count now in force."""
+    lib().oracle_set_threads(int(threads))
+    return int(lib().oracle_max_threads())

@@ -29,6 +29,8 @@ void oracle_masked_adam(float* param, const float* grad, float* exp_avg, float* 
     const float b1 = (float)beta1, a1 = (float)(1.0 - beta1), b2 = (float)beta2, a2 = (float)(1.0 - beta2);
     const float inv_bc2 = (float)(1.0 / bc2_sqrt), epsf = (float)eps, neg_ss = (float)(-step_size);
     const float wd = (float)weight_decay;
+    /* rows are independent: any thread split gives the same bits */
+#pragma omp parallel for schedule(static)
     for (long long r = 0; r < rows; r++) {
         if (relevant && !relevant[r]) continue;
         for (int j = 0; j < width; j++) {

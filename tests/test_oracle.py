@@ -115,3 +115,32 @@ def test_binning_oracle_matches_committed_fixture(name):
     ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + binning.bit_length_at_least_one(T))
     assert np.array_equal(ev, perm)
     assert np.array_equal(binning.tile_ranges(ek, T), ranges)
+
+
+@pytest.mark.parametrize("n,begin,end,threads", [(1, 0, 45, 4), (1000, 0, 39, 3), (300_000, 0, 45, 8),
+                                                 (200_000, 7, 51, 5), (50_000, 0, 64, 2), (10_000, 32, 32, 4)])
+def test_omp_sort_oracle_equals_numpy_definition(oracle_lib, n, begin, end, threads):
+    """The multi-threaded radix sort (the binning CPU baseline) is the same stable sort as the
+    numpy definition, whatever the thread count, with heavy key ties."""
+    g = np.random.default_rng(n + begin)
+    keys = (g.integers(0, 64, n).astype(np.uint64) << np.uint64(32)) | g.integers(0, 50, n).astype(np.uint64)
+    keys ^= g.integers(0, 2, n).astype(np.uint64) << np.uint64(63)
+    vals = np.arange(n, dtype=np.uint32)
+    ek, ev = binning.stable_sort_pairs(keys, vals, begin, end)
+    ko, vo = oracle_lib.sort_pairs_omp(keys, vals, begin, end, threads)
+    assert np.array_equal(ko, ek) and np.array_equal(vo, ev)
+
+
+def test_omp_adam_oracle_independent_of_threads(oracle_lib):
+    g = np.random.default_rng(3)
+    p0, g0 = g.standard_normal((5000, 7), dtype=np.float32), g.standard_normal((5000, 7), dtype=np.float32)
+    rel = g.random(5000) < 0.5
+    outs = []
+    before = oracle_lib.set_threads(0)
+    for th in (1, 6):
+        assert oracle_lib.set_threads(th) == th
+        p, m, v = p0.copy(), np.zeros_like(p0), np.zeros_like(p0)
+        oracle_lib.masked_adam(p, g0.copy(), m, v, rel, 1e-3, 0.9, 0.999, 1e-15, 0.0, 3)
+        outs.append(p)
+    oracle_lib.set_threads(before)
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
