@@ -1,36 +1,40 @@
 """bench.py -- BASELINE.json metric: fwd+bwd iters/s and HBM GB/s at 2M Gaussians, 1920x1080.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-(N > 1: launched by torch.distributed.run, one rank per GPU, RCCL backend.)
+  N > 1 without a torch.distributed environment: this process starts
+  `python -m torch.distributed.run --nproc-per-node N ... bench.py` as a child (before touching
+  any GPU), relays rank 0's JSON line and exits with the child's status.  Under the driver's
+  own torch.distributed.run launch the ranks are already there.  --backend gloo runs the
+  multi-rank plumbing on CPU (the exchange leg only; tests/test_bench.py).
 
-The headline metric needs the rasterizer forward + backward, whose kernels are not built
-("Decisions in force"), so `value` is null -- never estimated.  What the repo
-does build on this path is measured for real, at the configuration the metric is quoted
-on (config 3: 2M Gaussians, one 1920x1080 view, synthetic D2 inputs resident in HBM):
+The headline metric needs the rasterizer forward + backward, whose kernels were refused
+("Decisions in force"), so `value` is null -- never estimated.  What the repo builds
+on this path is measured for real, at the configuration the metric is quoted on (config 3:
+2M Gaussians, one 1920x1080 view per rank, synthetic D2 scene resident in HBM):
 
-  step      = the binning stage of one view: inclusive scan of the 2M tiles_touched,
-              stable radix sort of the K ~ 8M (tile|depth, id) pairs over bits
-              [0, 32 + getHigherMsb(8160)) = [0, 45) and the tile ranges, as one
-              hidegs_sort_tile_pairs call (rasterizer_impl.cu:321-371).
-              W warm-up steps, then K timed steps between HIP events on the launch stream,
-              barrier + synchronize on both sides, max over ranks.
-  roofline  = the dominant kernel of the step (the most time per step): 24 algorithmic
-              bytes per pair per launch for a sort pass (key 8 + value 4, read and written once), averaged
-              over its launches with per-launch HIP events (hidegs_kernel_timing), against
-              8 TB/s; traffic from the committed rocprofv3 PMC summary when present.
-  distCUDA2 = simple_knn._C.distCUDA2 on the 2M D2 centres (once-per-scene initialiser).
-  config5_scale = the same binning step and distCUDA2 at config 5's size (10M Gaussians, 4K frame).
-  exchange  = the view-DP exchange of 2M x 59 fp32 leaf gradients + stats over RCCL
-              (a one-rank group at N = 1), HIP-event timed.
-  exchange_and_step = the exchange followed by the masked step, in sequence and overlapped bucket
-              by bucket (ViewDPExchange.exchange_and_step); at N = 1 neither exchanges anything.
-  masked Adam = the fused row-masked optimizer step (hidegs_amd.optim.Adam, the OurAdam
-              drop-in) over the six HiDeGS parameter groups at 2M Gaussians (59 fp32 each), 90%
-              of rows visible; 28 algorithmic bytes per updated value; beside it the reference's
-              own op sequence (OurAdam.py:249-337 restated as torch ops) on the same GPU.
-  cpu_baseline = the oracle's stable sort (numpy, one core) on the same 8M pairs; beside the
-              distCUDA2 and masked Adam lines, the oracle's brute force on a sample of queries and
-              its masked Adam step.
+  step      = the binning stage of the rank's view: inclusive scan of the 2M tiles_touched
+              and one hidegs_sort_tile_pairs call -- the stable radix sort of the K ~ 8.6M
+              (tile | depth, id) pairs over [0, 32 + getHigherMsb(8160)) = [0, 45) plus the
+              tile ranges (rasterizer_impl.cu:321-371).  Pairs from D2's own screen-space
+              footprints (synthetic.d2_binning_workload).  W warm-up steps, then K timed steps
+              between HIP events on the launch stream, barrier + synchronize on both sides,
+              max over ranks.
+  roofline  = the dominant kernel of the step: 24 algorithmic bytes per pair per sort-pass
+              launch (key 8 + value 4, read and written once), averaged over its launches with
+              per-launch HIP events (hidegs_kernel_timing), against 8 TB/s; traffic from the
+              committed rocprofv3 PMC summary (profiles/latest_kernels.json).
+  binning_skewed = the same step on a view whose Gaussians crowd into hot tiles (15% of them in
+              a small disc: ~70 tiles over 8192 pairs take the partition queue).
+  distCUDA2 = simple_knn._C.distCUDA2 on the 2M D2 centres, with its issue-rate roofline (VALU
+              wave-instructions per second from the committed PMC summary, against the chip's).
+  config5_scale = the binning step and distCUDA2 at config 5's size (10M Gaussians, 4K frame).
+  exchange  = the view-DP exchange of 2M x 59 fp32 leaf gradients + stats over RCCL (no
+              collective at N = 1), HIP-event timed; algbw and ring busbw.
+  exchange_and_step = the exchange followed by the masked step, sequential and overlapped.
+  masked Adam = the fused row-masked optimizer step at 2M Gaussians (59 fp32 each), 90% visible.
+  cpu_baseline = on rank 0 at N = 1, every CPU leg on the same `cores` threads (the box's CPU
+              share, OMP_NUM_THREADS): the oracle's OpenMP stable radix sort of the same pairs
+              (headline), its kNN brute force on sampled queries, its masked Adam step.
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -47,8 +51,12 @@ import time
 N_GAUSSIANS = 2_000_000
 W_PX, H_PX = 1920, 1080
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 fp32 VALU instruction per SIMD per 2 cycles at 2.4 GHz
+VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2
 ROOT = os.path.dirname(os.path.abspath(__file__))
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "latest_kernels.json")  # tools/prof_summary.py output
+KNN_PMC_FILE = os.path.join(ROOT, "profiles", "latest_knn_pmc.json")   # tools/pmc_knn_valu.sh output
+SKEW_CLUSTER = (0.15, 0.1)
 
 
 def free_port() -> int:
@@ -70,17 +78,55 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def main() -> None:
+def cpu_threads() -> int:
+    """The CPU legs' thread count: the box's CPU share (OMP_NUM_THREADS, 16 on the GPU box), else
+    every core this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--knn-steps", type=int, default=5)
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="gloo: CPU ranks, the exchange leg only (plumbing tests)")
+    ap.add_argument("--n-gaussians", type=int, default=N_GAUSSIANS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exchange", action="store_true")
     ap.add_argument("--no-adam", action="store_true")
     ap.add_argument("--no-config5", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--no-skewed", action="store_true")
+    return ap.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """Start N ranks as a child torch.distributed.run (nothing here has touched a GPU) and relay
+    rank 0's JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")]
+    for ln in lines[-1:]:
+        print(ln, flush=True)
+    if proc.returncode == 0 and not lines:
+        print("bench.py: the ranks printed no result line", file=sys.stderr)
+        return 1
+    return proc.returncode
+
+
+def main() -> None:
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
 
     # The contract is ONE JSON line on stdout; RCCL prints a version banner there at init, so the
     # process's fd 1 goes to stderr for the run and the result line is written to the saved fd.
@@ -92,22 +138,28 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
-    import simple_knn
-    from hidegs_amd import _lib, primitives, synthetic
-    from hidegs_amd.view_dp import GradArena, ViewDPExchange
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    gpu = args.backend == "nccl"
+    if gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
     if not dist.is_initialized():
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ["MASTER_PORT"] = str(free_port())
-            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-        else:
-            dist.init_process_group("nccl", device_id=dev)
+        kw = {"device_id": dev} if gpu else {}
+        dist.init_process_group(args.backend, rank=rank, world_size=world, **kw)
+
+    from hidegs_amd import synthetic
+    from hidegs_amd.view_dp import GradArena, ViewDPExchange
+
+    N = args.n_gaussians
 
     def max_over_ranks(x: float) -> float:
         t = torch.tensor([x], device=dev, dtype=torch.float64)
@@ -115,70 +167,25 @@ def main() -> None:
         return float(t)
 
     def timed(fn, steps, warmup):
+        """(device ms per step from events on the current stream, wall ms per step), max over ranks."""
         for _ in range(warmup):
             fn()
         dist.barrier()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if gpu:
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
-        e0.record()
+        if gpu:
+            e0.record()
         for _ in range(steps):
             fn()
-        e1.record()
-        torch.cuda.synchronize()
+        if gpu:
+            e1.record()
+            torch.cuda.synchronize()
         dist.barrier()
-        wall = time.perf_counter() - t0
-        return max_over_ranks(e0.elapsed_time(e1) / steps), max_over_ranks(wall * 1e3 / steps)
-
-    # ---- the step: binning of one view (rank r renders its own view: seed r) -------------
-    wl = synthetic.binning_workload(N_GAUSSIANS, W_PX, H_PX, seed=rank, device=dev)
-    K, T = wl.num_pairs, wl.num_tiles
-    end_bit = 32 + primitives.higher_msb(T)
-    offsets = torch.empty_like(wl.tiles_touched)
-
-    def step():
-        primitives.inclusive_scan_u32(wl.tiles_touched, out=offsets)
-        primitives.sort_tile_pairs(wl.keys, wl.values, T)  # SortPairs + identifyTileRanges in one call
-
-    ms_step, wall_ms_step = timed(step, args.steps, args.warmup)
-
-    # per-kernel durations of the same step, live, with per-launch HIP events
-    kt_steps = max(10, min(args.steps, 50))
-    # algorithmic bytes per launch (SURVEY §8(d) D4 per-pair figures: a sort pass reads and writes
-    # key 8 + value 4; a histogram or range pass reads the 8-byte keys; the scan reads and writes u32)
-    alg = {"scan_reduce": 4 * N_GAUSSIANS, "scan_small": 0, "scan_downsweep": 8 * N_GAUSSIANS,
-           "radix_hist_u64": 8 * K, "radix_digit_scan": 0, "radix_scatter_u64": 24 * K,
-           "segment_ranges": 0,  # ranges from the digit counts: a few partial tiles, not the keys
-           "segment_sort": 24 * K, "identify_ranges": 8 * K,
-           "big_segments": 0}  # the hot-tile queue: no tile over 24576 pairs here, so it only checks and exits
-    with _lib.kernel_timer() as kt:
-        for _ in range(kt_steps):
-            step()
-        torch.cuda.synchronize()
-        kern = {}
-        for nm, nbytes in alg.items():
-            ms, n = kt.get(nm)
-            if n == 0:
-                continue
-            avg_us = ms * 1e3 / n
-            kern[nm] = {"avg_us": round(avg_us, 2), "launches_per_step": n // kt_steps,
-                        "us_per_step": round(ms * 1e3 / kt_steps, 2),
-                        "GBps": round(nbytes / (avg_us * 1e-6) / 1e9, 1) if nbytes else None}
-    dom = max((k for k in kern if alg[k]), key=lambda k: kern[k]["us_per_step"])
-    dom_us = kern[dom]["avg_us"]
-    dom_bytes = alg[dom]
-    achieved = dom_bytes / (dom_us * 1e-6) / 1e9
-    traffic = None
-    rocprof_name = {"radix_scatter_u64": "radix_scatter_kernel", "segment_sort": "segment_sort_kernel",
-                    "radix_hist_u64": "radix_hist_kernel"}.get(dom, dom + "_kernel")
-    # launch grid (threads) the rocprof summary keys the kernel by: one workgroup per tile (T) or per
-    # 4096-pair tile of the sort (the scatter runs 512-thread workgroups, the others 256)
-    ntiles_sort = (K + 4095) // 4096
-    grid = {"segment_sort": T * 256, "radix_scatter_u64": ntiles_sort * 512}.get(dom, ntiles_sort * 256)
-    if os.path.exists(TRAFFIC_FILE):
-        with open(TRAFFIC_FILE) as f:
-            traffic = json.load(f).get(f"{rocprof_name}@{grid}", {}).get("hbm_bytes_per_launch")
-    sort_us = sum(kern[k]["us_per_step"] for k in kern if k.startswith(("radix_", "segment_")))
+        wall = (time.perf_counter() - t0) * 1e3 / steps
+        dev_ms = e0.elapsed_time(e1) / steps if gpu else wall
+        return max_over_ranks(dev_ms), max_over_ranks(wall)
 
     line = {
         "metric": "fwd+bwd iters/sec & HBM GB/s at 2M Gaussians, 1920x1080",
@@ -191,94 +198,190 @@ def main() -> None:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u64/u32 (binning), f32 (distCUDA2, exchange)",
-        "data": "synthetic (SURVEY §8(d) D2, seeded per rank)",
+        "dtype": "u64/u32 (binning), f32 (distCUDA2, exchange, masked Adam)",
+        "data": "synthetic (SURVEY §8(d) D2 scene, seeded per rank)",
         "config": {"workload": "config 3: 2M Gaussians, 1920x1080, one view per rank -- binning stage, "
-                               "distCUDA2 and the view-DP exchange measured; rasterizer fwd/bwd not built",
-                   "n_gaussians": N_GAUSSIANS, "width": W_PX, "height": H_PX, "tiles": T, "pairs_K": K,
-                   "sort_bits": [0, end_bit], "parallelism": f"view-dp{world}"},
-        "status": "headline UNMEASURED: the rasterizer forward/backward kernels are not built "
+                               "distCUDA2, the view-DP exchange and the masked step measured; rasterizer "
+                               "fwd/bwd refused (not built)",
+                   "n_gaussians": N, "width": W_PX, "height": H_PX, "parallelism": f"view-dp{world}",
+                   "backend": "rccl" if gpu else "gloo"},
+        "status": "headline UNMEASURED: the rasterizer forward/backward kernels were refused "
                   "(DESIGN.md, 'Decisions in force'); value stays null",
-        "binning_step": {"ms_per_step": round(ms_step, 4), "wall_ms_per_step": round(wall_ms_step, 4),
-                         "pairs_per_s_all_ranks": K * world / (ms_step * 1e-3),
-                         "views_per_s_all_ranks": world / (ms_step * 1e-3),
-                         "sort_us": round(sort_us, 2), "kernels": kern},
-        "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
-                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": dom_us},
+        "roofline": None,
         "cpu_baseline": None,
     }
+    cam = synthetic.d2_camera(W_PX, H_PX)
+    scene = synthetic.d2_scene(N, cam, seed=rank)
 
-    # ---- distCUDA2 at 2M ---------------------------------------------------------------------
-    pts = synthetic.frustum_points(N_GAUSSIANS, seed=rank).to(dev)
+    ctx = {}
+    if gpu:
+        _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch)
+    if not args.no_exchange:
+        _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, GradArena, ViewDPExchange)
+    if gpu and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        _cpu_baselines(line, ctx, N, cam, np)
+
+    dist.destroy_process_group()
+    sys.stdout.flush()
+    if rank == 0:
+        os.write(result_fd, (json.dumps(line) + "\n").encode())
+
+
+def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
+    import simple_knn
+    from hidegs_amd import _lib, primitives, synthetic
+
+    N = scene.n
+    # ---- the step: binning of one view (rank r renders its own view: seed r) -------------------
+    wl = synthetic.d2_binning_workload(scene, cam, device=dev)
+    K, T = wl.num_pairs, wl.num_tiles
+    end_bit = 32 + primitives.higher_msb(T)
+    offsets = torch.empty_like(wl.tiles_touched)
+    V = int((wl.tiles_touched > 0).sum())
+    line["config"].update({"tiles": T, "pairs_K": K, "visible_V": V, "pixels_Px": cam.width * cam.height,
+                           "sort_bits": [0, end_bit]})
+
+    def make_step(w):
+        off = torch.empty_like(w.tiles_touched)
+
+        def step():
+            primitives.inclusive_scan_u32(w.tiles_touched, out=off)
+            primitives.sort_tile_pairs(w.keys, w.values, w.num_tiles)  # SortPairs + identifyTileRanges
+        return step
+
+    step = make_step(wl)
+    ms_step, wall_ms_step = timed(step, args.steps, args.warmup)
+    qerr = primitives.queue_error()
+
+    # per-kernel durations of the same step, live, with per-launch HIP events on the launch stream
+    kt_steps = max(10, min(args.steps, 50))
+    # algorithmic bytes per launch (SURVEY §8(d) D4 per-pair figures: a sort pass reads and writes
+    # key 8 + value 4; a histogram pass reads the 8-byte keys; the scan reads and writes u32)
+    alg = {"scan_reduce": 4 * N, "scan_small": 0, "scan_downsweep": 8 * N,
+           "radix_hist_u64": 8 * K, "radix_digit_scan": 0, "radix_scatter_u64": 24 * K,
+           "segment_sort": 24 * K, "big_segments": 0}
+
+    def kernel_table(fn, nsteps):
+        with _lib.kernel_timer() as kt:
+            for _ in range(nsteps):
+                fn()
+            torch.cuda.synchronize()
+            kern = {}
+            for nm, nbytes in alg.items():
+                ms, n = kt.get(nm)
+                if n == 0:
+                    continue
+                avg_us = ms * 1e3 / n
+                kern[nm] = {"avg_us": round(avg_us, 2), "launches_per_step": n // nsteps,
+                            "us_per_step": round(ms * 1e3 / nsteps, 2),
+                            "GBps": round(nbytes / (avg_us * 1e-6) / 1e9, 1) if nbytes else None}
+        return kern
+
+    kern = kernel_table(step, kt_steps)
+    dom = max((k for k in kern if alg[k]), key=lambda k: kern[k]["us_per_step"])
+    dom_us = kern[dom]["avg_us"]
+    dom_bytes = alg[dom]
+    achieved = dom_bytes / (dom_us * 1e-6) / 1e9
+    traffic = None
+    rocprof_name = {"radix_scatter_u64": "radix_scatter_kernel", "segment_sort": "segment_sort_kernel",
+                    "radix_hist_u64": "radix_hist_kernel"}.get(dom, dom + "_kernel")
+    ntiles_sort = (K + 4095) // 4096
+    grid = {"segment_sort": (T + 16) * 256, "radix_scatter_u64": ntiles_sort * 512}.get(dom, ntiles_sort * 256)
+    traffic_src = f"{rocprof_name}@{grid}"
+    if os.path.exists(TRAFFIC_FILE):
+        with open(TRAFFIC_FILE) as f:
+            traffic = json.load(f).get(traffic_src, {}).get("hbm_bytes_per_launch")
+    sort_us = sum(kern[k]["us_per_step"] for k in kern if k.startswith(("radix_", "segment_", "big_")))
+    line["binning_step"] = {"ms_per_step": round(ms_step, 4), "wall_ms_per_step": round(wall_ms_step, 4),
+                            "pairs_per_s_all_ranks": K * world / (ms_step * 1e-3),
+                            "views_per_s_all_ranks": world / (ms_step * 1e-3),
+                            "sort_us": round(sort_us, 2), "queue_error": qerr, "kernels": kern}
+    line["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                        "traffic": None if traffic is None else round(traffic),
+                        "traffic_profile": traffic_src, "algorithmic_bytes_per_launch": dom_bytes,
+                        "avg_launch_us": dom_us}
+    line["ms_per_step_binning"] = round(ms_step, 4)
+
+    # ---- the same step on a skewed view (hot tiles through the partition queue) ----------------
+    if not args.no_skewed:
+        sk_scene = synthetic.d2_scene(N, cam, seed=1000 + rank, cluster=SKEW_CLUSTER)
+        wls = synthetic.d2_binning_workload(sk_scene, cam, device=dev)
+        counts = torch.bincount((wls.keys >> 32).long(), minlength=wls.num_tiles)
+        sk_step = make_step(wls)
+        ms_sk, _ = timed(sk_step, max(20, args.steps // 4), 3)
+        qerr_sk = primitives.queue_error()
+        ksk = kernel_table(sk_step, 10)
+        line["binning_skewed"] = {"workload": f"D2 with {SKEW_CLUSTER[0]:.0%} of the Gaussians in a disc of NDC "
+                                              f"radius {SKEW_CLUSTER[1]}",
+                                  "pairs_K": wls.num_pairs, "max_tile_pairs": int(counts.max()),
+                                  "tiles_over_8192": int((counts > 8192).sum()),
+                                  "tiles_over_2048": int((counts > 2048).sum()),
+                                  "ms_per_step": round(ms_sk, 4), "queue_error": qerr_sk,
+                                  "kernels_us_per_step": {k: v["us_per_step"] for k, v in ksk.items()}}
+        del sk_scene, wls, counts
+
+    # ---- distCUDA2 at 2M -------------------------------------------------------------------------
+    pts = scene.means3D.to(dev)
     knn_ms, _ = timed(lambda: simple_knn._C.distCUDA2(pts), args.knn_steps, 1)
     with _lib.kernel_timer() as kt:
         simple_knn._C.distCUDA2(pts)
         torch.cuda.synchronize()
         kk = {nm: round(kt.get(nm)[0] * 1e3, 1) for nm in ("bounds", "morton", "radix_scatter_u64", "gather",
                                                              "leaf_box", "knn_leaf", "knn_hard")}
-    line["distCUDA2"] = {"points": N_GAUSSIANS, "ms": round(knn_ms, 3),
-                         "points_per_s_all_ranks": N_GAUSSIANS * world / (knn_ms * 1e-3), "kernels_us": kk,
-                         "algorithmic_bytes": 16 * N_GAUSSIANS,
-                         "hbm_frac": round(16 * N_GAUSSIANS / (knn_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
+    kd = {"points": N, "ms": round(knn_ms, 3), "points_per_s_all_ranks": N * world / (knn_ms * 1e-3),
+          "kernels_us": kk, "algorithmic_bytes": 16 * N,
+          "hbm_frac": round(16 * N / (knn_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
+    if os.path.exists(KNN_PMC_FILE):
+        with open(KNN_PMC_FILE) as f:
+            pmc = json.load(f)
+        leaf = pmc.get("knn_leaf_kernel")
+        if leaf and leaf.get("SQ_INSTS_VALU") and kk.get("knn_leaf"):
+            rate = leaf["SQ_INSTS_VALU"] / (kk["knn_leaf"] * 1e-6)
+            kd["issue_roofline"] = {"kernel": "knn_leaf", "bound": "valu-issue",
+                                    "valu_wave_instr_per_launch": leaf["SQ_INSTS_VALU"],
+                                    "achieved_wave_instr_per_s": rate, "peak_wave_instr_per_s": VALU_PEAK_WAVE_INSTR_PER_S,
+                                    "frac": round(rate / VALU_PEAK_WAVE_INSTR_PER_S, 4), "pmc_source": KNN_PMC_FILE[len(ROOT) + 1:]}
+    line["distCUDA2"] = kd
 
-    # ---- config 5's scale: 10M Gaussians, 3840x2160 frame ------------------------------------
+    # ---- config 5's scale: 10M Gaussians, 3840x2160 frame ----------------------------------------
     if not args.no_config5:
-        wl5 = synthetic.binning_workload(10_000_000, 3840, 2160, seed=rank, device=dev)
-        off5 = torch.empty_like(wl5.tiles_touched)
-
-        def step5():
-            primitives.inclusive_scan_u32(wl5.tiles_touched, out=off5)
-            primitives.sort_tile_pairs(wl5.keys, wl5.values, wl5.num_tiles)
-
+        cam5 = synthetic.d2_camera(3840, 2160)
+        sc5 = synthetic.d2_scene(10_000_000, cam5, seed=rank)
+        wl5 = synthetic.d2_binning_workload(sc5, cam5, device=dev)
+        step5 = make_step(wl5)
         ms5, _ = timed(step5, 20, 3)
-        pts5 = synthetic.frustum_points(10_000_000, seed=rank).to(dev)
+        pts5 = sc5.means3D.to(dev)
         knn5_ms, _ = timed(lambda: simple_knn._C.distCUDA2(pts5), 3, 1)
-        line["config5_scale"] = {"workload": "10M Gaussians, 3840x2160 (32400 tiles): binning step and distCUDA2",
+        line["config5_scale"] = {"workload": "10M D2 Gaussians, 3840x2160 (32400 tiles): binning step and distCUDA2",
                                  "binning_ms_per_step": round(ms5, 4), "pairs_K": wl5.num_pairs,
                                  "sort_bits": [0, 32 + primitives.higher_msb(wl5.num_tiles)],
                                  "pairs_per_s_all_ranks": wl5.num_pairs * world / (ms5 * 1e-3),
-                                 "distCUDA2_ms": round(knn5_ms, 3)}
-        del wl5, off5, pts5
+                                 "distCUDA2_ms": round(knn5_ms, 3), "queue_error": primitives.queue_error()}
+        del sc5, wl5, pts5
 
-    # ---- view-DP exchange at 2M ---------------------------------------------------------------
-    if not args.no_exchange:
-        g = torch.Generator(device=dev).manual_seed(rank)
-        visible = torch.rand(N_GAUSSIANS, device=dev, generator=g) < 0.9
-        arena = GradArena(N_GAUSSIANS, device=dev)
-        arena.flat.normal_(generator=g)
-        norm = torch.rand(N_GAUSSIANS, 1, device=dev, generator=g)
-        radii = torch.rand(N_GAUSSIANS, device=dev, generator=g)
-        ex = ViewDPExchange()
-        ex_ms, _ = timed(lambda: ex.exchange(arena, visible, max_stats=[norm, radii]), 20, 3)
-        line["exchange"] = {"ms_per_step": round(ex_ms, 3), "world": world, "grad_bytes_per_rank": ex.last.reduced_bytes,
-                            "algbw_GBps": ex.last.reduced_bytes / (ex_ms * 1e-3) / 1e9,
-                            "collectives_per_step": ex.last.collectives, "compacted": ex.last.compacted,
-                            "union_rows": ex.last.union_rows}
-
-    # ---- masked Adam at 2M ---------------------------------------------------------------------
+    # ---- masked Adam at 2M ------------------------------------------------------------------------
     if not args.no_adam:
         from hidegs_amd.optim import Adam
         widths = {"xyz": 3, "f_dc": 3, "f_rest": 45, "opacity": 1, "scaling": 3, "rotation": 4}
         lrs = {"xyz": 0.00016 * 4.2, "f_dc": 0.0025, "f_rest": 0.0025 / 20.0, "opacity": 0.025, "scaling": 0.005,
                "rotation": 0.001}
         g = torch.Generator(device=dev).manual_seed(100 + rank)
-        prm = {k: torch.nn.Parameter(torch.randn(N_GAUSSIANS, w, device=dev, generator=g)) for k, w in widths.items()}
+        prm = {k: torch.nn.Parameter(torch.randn(N, w, device=dev, generator=g)) for k, w in widths.items()}
         for p in prm.values():
             p.grad = torch.randn(p.shape, device=dev, generator=g)
-        vis = torch.rand(N_GAUSSIANS, device=dev, generator=g) < 0.9
-        opt = Adam([{"params": [prm[k]], "lr": lrs[k], "name": k} for k in widths], lr=0.0, eps=1e-15)
+        vis = torch.rand(N, device=dev, generator=g) < 0.9
+        opt = Adam([{"params": [prm[k]], "lr": lrs[k], "name": k} for k, w in widths.items()], lr=0.0, eps=1e-15)
         ad_ms, _ = timed(lambda: opt.step(vis), 20, 3)
         nvis = int(vis.sum())
-        ad_bytes = 28 * 59 * nvis + N_GAUSSIANS
+        ad_bytes = 28 * 59 * nvis + N
         with _lib.kernel_timer() as kt:
             opt.step(vis)
             torch.cuda.synchronize()
             k_ms, k_n = kt.get("masked_adam")
-        # the reference's op sequence on the same GPU (gather, 8 elementwise ops, scatter per parameter)
         st = {k: (torch.zeros_like(p), torch.zeros_like(p)) for k, p in prm.items()}
 
-        def ref_step():
+        def ref_step():  # the reference's op sequence on the same GPU (OurAdam.py:249-337)
             with torch.no_grad():
                 for k, parami in prm.items():
                     m_all, v_all = st[k]
@@ -291,85 +394,102 @@ def main() -> None:
                     v_all[vis] = exp_avg_sq
                     parami[vis] = param
         ref_ms, _ = timed(ref_step, 5, 1)
-        line["masked_adam"] = {"gaussians": N_GAUSSIANS, "visible_rows": nvis, "ms": round(ad_ms, 4),
+        line["masked_adam"] = {"gaussians": N, "visible_rows": nvis, "ms": round(ad_ms, 4),
                                "kernel_us_total": round(k_ms * 1e3, 1), "launches": k_n,
                                "algorithmic_bytes": ad_bytes, "GBps": round(ad_bytes / (ad_ms * 1e-3) / 1e9, 1),
                                "hbm_frac": round(ad_bytes / (ad_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                                "reference_torch_ops_ms": round(ref_ms, 3),
                                "speedup_vs_reference_ops": round(ref_ms / ad_ms, 2)}
-        # the exchange and the step after it, in sequence and overlapped bucket by bucket
-        if not args.no_exchange:
-            arena = GradArena(N_GAUSSIANS, device=dev)
-            for k, p in prm.items():
-                arena[k].copy_(p.grad)
-            arena.attach(prm)
-            ex = ViewDPExchange()
-            norm = torch.rand(N_GAUSSIANS, 1, device=dev, generator=g)
+        ctx["adam_state"] = (prm, opt, vis, g)
+    ctx["binning_pairs"] = (wl, end_bit, sort_us)
 
-            def seq_step():
-                res = ex.exchange(arena, vis, max_stats=[norm])
-                opt.step(res.union)
 
-            seq_ms, _ = timed(seq_step, 10, 2)
-            fused_ms, _ = timed(lambda: ex.exchange_and_step(arena, vis, opt, prm, max_stats=[norm]), 10, 2)
-            line["exchange_and_step"] = {"world": world, "sequential_ms": round(seq_ms, 3),
-                                         "overlapped_ms": round(fused_ms, 3),
-                                         "collectives": ex.last.collectives, "union_rows": ex.last.union_rows}
-            del arena
-        del prm, opt, st
+def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, GradArena, ViewDPExchange):
+    g = torch.Generator(device=dev).manual_seed(rank)
+    visible = torch.rand(N, device=dev, generator=g) < 0.9
+    arena = GradArena(N, device=dev)
+    arena.flat.normal_(generator=g)
+    norm = torch.rand(N, 1, device=dev, generator=g)
+    radii = torch.rand(N, device=dev, generator=g)
+    ex = ViewDPExchange()
+    reps = 20 if gpu else 3
+    ex_ms, ex_wall = timed(lambda: ex.exchange(arena, visible, max_stats=[norm, radii]), reps, 2)
+    nbytes = ex.last.reduced_bytes
+    algbw = nbytes / (ex_ms * 1e-3) / 1e9 if nbytes else None
+    line["exchange"] = {"ms_per_step": round(ex_ms, 3), "wall_ms_per_step": round(ex_wall, 3), "world": world,
+                        "timing": "HIP events on the compute stream (it waits for every RCCL bucket)" if gpu
+                        else "wall clock (gloo, CPU)",
+                        "grad_bytes_per_rank": nbytes, "algbw_GBps": algbw,
+                        "busbw_GBps": None if algbw is None else algbw * 2 * (world - 1) / world,
+                        "collectives_per_step": ex.last.collectives, "compacted": ex.last.compacted,
+                        "union_rows": ex.last.union_rows}
+    st = ctx.get("adam_state")
+    if st is not None:
+        prm, opt, vis, g2 = st
+        arena2 = GradArena(N, device=dev)
+        for k, p in prm.items():
+            arena2[k].copy_(p.grad)
+        arena2.attach(prm)
+        ex2 = ViewDPExchange()
+        norm2 = torch.rand(N, 1, device=dev, generator=g2)
 
-    # ---- CPU baseline (rank 0, N = 1): the oracle's stable sort on the same pairs -------------
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import binning
-        keys = wl.keys.cpu().numpy().view(np.uint64)
-        vals = wl.values.cpu().numpy().view(np.uint32)
-        reps, t0 = 0, time.perf_counter()
-        while reps < 3 or (time.perf_counter() - t0 < 10.0 and reps < 20):
-            binning.stable_sort_pairs(keys, vals, 0, end_bit)
-            reps += 1
-        dt = (time.perf_counter() - t0) / reps
-        line["cpu_baseline"] = {"value": K / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
-                                "sample": f"stable sort of the same {K} (key, value) pairs over bits [0,{end_bit}) "
-                                          f"(numpy argsort kind=stable + gather, oracle/binning.py), {reps} reps",
-                                "cpu": cpu_model(), "gpu_speedup_sort": round(dt * 1e3 / (sort_us * 1e-3), 1)}
-        import oracle
-        omp = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-        # distCUDA2: the oracle's brute force (OpenMP) for a sample of the 2M D2 queries, each
-        # against all 2M points
-        if "distCUDA2" in line:
-            cpu_pts = synthetic.frustum_points(N_GAUSSIANS, seed=rank).numpy()
-            nq = 256
-            idx = np.random.default_rng(0).choice(N_GAUSSIANS, nq, replace=False)
+        def seq_step():
+            res = ex2.exchange(arena2, vis, max_stats=[norm2], params=prm)
+            opt.step(res.union)
+
+        seq_ms, _ = timed(seq_step, 10, 2)
+        fused_ms, _ = timed(lambda: ex2.exchange_and_step(arena2, vis, opt, prm, max_stats=[norm2]), 10, 2)
+        line["exchange_and_step"] = {"world": world, "sequential_ms": round(seq_ms, 3),
+                                     "overlapped_ms": round(fused_ms, 3),
+                                     "collectives": ex2.last.collectives, "union_rows": ex2.last.union_rows}
+
+
+def _cpu_baselines(line, ctx, N, cam, np):
+    import oracle
+    from hidegs_amd import synthetic
+    threads = oracle.set_threads(cpu_threads())
+    info = {"cpu": cpu_model(), "cores": threads, "host_cpu_count": os.cpu_count()}
+    wl, end_bit, sort_us = ctx["binning_pairs"]
+    keys = wl.keys.cpu().numpy().view(np.uint64)
+    vals = wl.values.cpu().numpy().view(np.uint32)
+    K = keys.size
+    reps, t0 = 0, time.perf_counter()
+    while reps < 3 or (time.perf_counter() - t0 < 10.0 and reps < 30):
+        oracle.sort_pairs_omp(keys, vals, 0, end_bit, threads)
+        reps += 1
+    dt = (time.perf_counter() - t0) / reps
+    line["cpu_baseline"] = {"value": K / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+                            "sample": f"stable sort of the same {K} (key, value) pairs over bits [0,{end_bit}) "
+                                      f"(oracle/sort_ref.c, OpenMP radix sort on {threads} threads), {reps} reps",
+                            **info, "gpu_speedup_sort": round(dt * 1e3 / (sort_us * 1e-3), 1)}
+    # distCUDA2: the oracle's brute force for a sample of the 2M D2 queries, each against all points
+    if "distCUDA2" in line:
+        cpu_pts = synthetic.d2_scene(N, cam, seed=0).means3D.numpy()
+        nq = 64 * threads
+        idx = np.random.default_rng(0).choice(N, nq, replace=False)
+        t0 = time.perf_counter()
+        oracle.knn_mean3_subset(cpu_pts, idx)
+        dq = time.perf_counter() - t0
+        line["distCUDA2"]["cpu_baseline"] = {
+            "value": nq / dq, "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{nq} of the {N} D2 queries, each brute-forced against all points (oracle/knn_ref.c, OpenMP)",
+            "gpu_queries_per_s": line["distCUDA2"]["points_per_s_all_ranks"]}
+        del cpu_pts
+    # masked Adam: the oracle's restatement (oracle/adam_ref.c, OpenMP over rows), one full step
+    if "masked_adam" in line:
+        rng = np.random.default_rng(1)
+        rel = rng.random(N) < 0.9
+        t_total = 0.0
+        for w in (3, 3, 45, 1, 3, 4):
+            pa = rng.standard_normal((N, w), dtype=np.float32)
+            ga = rng.standard_normal((N, w), dtype=np.float32)
+            ma, va = np.zeros_like(pa), np.zeros_like(pa)
             t0 = time.perf_counter()
-            oracle.knn_mean3_subset(cpu_pts, idx)
-            dq = time.perf_counter() - t0
-            line["distCUDA2"]["cpu_baseline"] = {
-                "value": nq / dq, "unit": "queries/s", "cores": omp, "kind": "port",
-                "sample": f"{nq} of the {N_GAUSSIANS} D2 queries, each brute-forced against all points "
-                          "(oracle/knn_ref.c, OpenMP)",
-                "gpu_queries_per_s": line["distCUDA2"]["points_per_s_all_ranks"]}
-            del cpu_pts
-        # masked Adam: the oracle's restatement (oracle/adam_ref.c, one core) of one step over the
-        # same six 2M-row parameter groups, 90% of rows relevant
-        if "masked_adam" in line:
-            rng = np.random.default_rng(1)
-            rel = rng.random(N_GAUSSIANS) < 0.9
-            t_total = 0.0
-            for w in (3, 3, 45, 1, 3, 4):
-                pa = rng.standard_normal((N_GAUSSIANS, w), dtype=np.float32)
-                ga = rng.standard_normal((N_GAUSSIANS, w), dtype=np.float32)
-                ma, va = np.zeros_like(pa), np.zeros_like(pa)
-                t0 = time.perf_counter()
-                oracle.masked_adam(pa, ga, ma, va, rel, 1e-3, 0.9, 0.999, 1e-15, 0.0, 1)
-                t_total += time.perf_counter() - t0
-            line["masked_adam"]["cpu_baseline"] = {
-                "value": 1e3 * t_total, "unit": "ms per step", "cores": 1, "kind": "port",
-                "sample": f"one full step, {N_GAUSSIANS} Gaussians x 59 floats, 90% of rows relevant"}
-
-    dist.destroy_process_group()
-    sys.stdout.flush()
-    if rank == 0:
-        os.write(result_fd, (json.dumps(line) + "\n").encode())
+            oracle.masked_adam(pa, ga, ma, va, rel, 1e-3, 0.9, 0.999, 1e-15, 0.0, 1)
+            t_total += time.perf_counter() - t0
+        line["masked_adam"]["cpu_baseline"] = {
+            "value": 1e3 * t_total, "unit": "ms per step", "cores": threads, "kind": "port",
+            "sample": f"one full step, {N} Gaussians x 59 floats, 90% of rows relevant (oracle/adam_ref.c, OpenMP)"}
 
 
 if __name__ == "__main__":
