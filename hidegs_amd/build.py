@@ -36,6 +36,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=o
 # tag -> (extra defines, the sources they change); the other objects are shared with the product build
 VARIANTS = {
     "qcap": (["-DHIDEGS_JOB_CAP=64"], ["primitives.hip"]),  # partition-queue overflow -> error word
+    "gform": (["-DHIDEGS_QUEUE_MIN=8192"], ["primitives.hip"]),  # tiles of 2049..8192 pairs: one-workgroup global form
 }
 
 

@@ -827,7 +827,8 @@ constexpr int kQueueBlocks = HIDEGS_QUEUE_BLOCKS;
 #define HIDEGS_BACKOFF_MAX 16  // a waiting worker's longest sleep between polls, in s_sleep(8) units
 #endif
 #ifndef HIDEGS_QUEUE_MIN
-#define HIDEGS_QUEUE_MIN 8192  // segments up to this many pairs: the one-workgroup global form
+#define HIDEGS_QUEUE_MIN 2048  // segments up to this many pairs: the one-workgroup global form (2048 = kSegCap:
+                              // every tile over kSegCap goes to the queue; tools/skew_time.py A/B in DESIGN.md)
 #endif
 constexpr int kQueueMin = HIDEGS_QUEUE_MIN;
 constexpr uint32_t kMaxPolls = 1u << 22;
@@ -1306,13 +1307,16 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
 #endif
 constexpr int kOpenLocal = HIDEGS_OPEN_LOCAL;
 #ifndef HIDEGS_SCATTER_LOCAL
-#define HIDEGS_SCATTER_LOCAL 16384  // ... and up to this many, its SCATTER phase too
+#define HIDEGS_SCATTER_LOCAL 8192  // ... and up to this many, its SCATTER phase too
 #endif
 constexpr int kScatterLocal = HIDEGS_SCATTER_LOCAL;
 #ifndef HIDEGS_SCOUTS
-#define HIDEGS_SCOUTS 16  // segment_sort_kernel's first workgroups, which start the hot tiles (0: own workgroup)
+#define HIDEGS_SCOUTS 128  // segment_sort_kernel's first workgroups, which start the hot tiles (0: own workgroup)
 #endif
 constexpr int kScouts = HIDEGS_SCOUTS;
+constexpr int kScoutItems = 32;  // segments per scout thread per sweep (a sweep: 8192 segments)
+// a scout's share of one sweep's hot tiles fits its kBlock-entry list
+static_assert(kScouts == 0 || kBlock * kScoutItems <= kScouts * kBlock, "HIDEGS_SCOUTS: at least 32 scouts (or 0)");
 __device__ __forceinline__ void open_local(const uint64_t* keys, const uint32_t* vals, const BigQueue& q,
                                            const uint32_t begin,
                                            const uint32_t m, BigShared& sh, EmitShared& e, uint32_t* s_and,
@@ -1402,14 +1406,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
     if (kScouts > 0 && blockIdx.x < (unsigned)kScouts) {
         // a scout: the first workgroups dispatched find the hot tiles (over kQueueMin pairs) and start
         // them -- the local phases of open_local, or a queue record -- while the other workgroups sort
-        // the ordinary tiles, instead of wherever in the grid the hot tile's own workgroup would run
+        // the ordinary tiles, instead of wherever in the grid the hot tile's own workgroup would run.
+        // Every scout sweeps all segments and numbers the hot ones the same way (thread-major within a
+        // sweep); scout b takes the hot tiles numbered b mod kScouts, so the hot tiles of one image
+        // region -- neighbouring segment ids -- are opened side by side, not by one scout in turn
+        // (71 hot tiles of a skewed view: 1.13 ms of segment_sort with 16 scouts of 256-segment stripes)
         uint32_t* list = lds.queue.list;
-        for (uint32_t s0 = blockIdx.x * kBlock; s0 < (uint32_t)nseg; s0 += kScouts * kBlock) {
+        uint32_t carry = 0u;  // hot tiles numbered in earlier sweeps
+        for (uint32_t s0 = 0; s0 < (uint32_t)nseg; s0 += kBlock * kScoutItems) {
             if (threadIdx.x == 0) lds.queue.nlist = 0u;
-            __syncthreads();
-            const uint32_t sg = s0 + threadIdx.x;
-            if (sg < (uint32_t)nseg && starts[sg + 1] - starts[sg] > (uint32_t)kQueueMin)
-                list[atomicAdd(&lds.queue.nlist, 1u)] = sg;
+            uint32_t hot = 0u;  // bit u: segment s0 + u * kBlock + threadIdx.x is hot
+#pragma unroll 8
+            for (int u = 0; u < kScoutItems; u++) {
+                const uint32_t sg = s0 + (uint32_t)u * kBlock + threadIdx.x;
+                if (sg < (uint32_t)nseg && starts[sg + 1] - starts[sg] > (uint32_t)kQueueMin) hot |= 1u << u;
+            }
+            uint32_t nhot;
+            const uint32_t base = carry + block_exclusive_scan((uint32_t)__builtin_popcount(hot), s_max, &nhot);
+            carry += nhot;  // block-uniform
+            if (nhot == 0u) continue;
+            uint32_t ord = base;
+            for (uint32_t h = hot; h; h &= h - 1u, ord++)
+                if (ord % (uint32_t)kScouts == blockIdx.x)
+                    list[atomicAdd(&lds.queue.nlist, 1u)] = s0 + (uint32_t)__builtin_ctz(h) * kBlock + threadIdx.x;
             __syncthreads();
             const uint32_t nl = lds.queue.nlist;  // workgroup-uniform
             for (uint32_t j = 0; j < nl; j++) {

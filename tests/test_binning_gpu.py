@@ -363,6 +363,66 @@ def test_segment_starts_edge_cases(case):
     assert torch.equal(ko2, ko) and torch.equal(vo2, vo)
 
 
+def _variant_sort_tile_pairs(var, kd, vd, T):
+    """hidegs_sort_tile_pairs of another build of the library (build.VARIANTS) -> (rc, keys, values, ranges)."""
+    from hidegs_amd import _lib
+    n = kd.numel()
+    dev = kd.device
+    ko, vo = torch.empty_like(kd), torch.empty_like(vd)
+    rng = torch.empty((T, 2), dtype=torch.int32, device=dev)
+    tmp = torch.empty(int(var.hidegs_sort_pairs_u64_scratch_bytes(n)), dtype=torch.uint8, device=dev)
+    rc = var.hidegs_sort_tile_pairs(_lib.ptr(tmp), tmp.numel(), _lib.ptr(kd), _lib.ptr(ko), _lib.ptr(vd),
+                                    _lib.ptr(vo), n, T, _lib.ptr(rng), _lib.stream_handle(dev))
+    return rc, ko, vo, rng
+
+
+def _many_hot_tiles(T, K, sizes, seed):
+    """K ordinary pairs over T tiles plus one tile of each size in `sizes` (tiles spread over the grid,
+    depths uniform), shuffled: Gaussian-major order is irrelevant to a stable sort's contract."""
+    g = np.random.default_rng(seed)
+    keys, _ = raster_like_keys(K, T, seed)
+    tiles = g.choice(T, len(sizes), replace=False).astype(np.uint64)
+    hot = [(tiles[i] << np.uint64(32)) | g.uniform(0.5, 60.0, s).astype(np.float32).view(np.uint32).astype(np.uint64)
+           for i, s in enumerate(sizes)]
+    keys = np.concatenate([keys] + hot)
+    keys = keys[g.permutation(keys.size)]
+    return keys, np.arange(keys.size, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("T,count,lo,hi", [(8160, 300, 2049, 9000), (32400, 200, 2049, 30000), (8160, 40, 20000, 60000)])
+def test_many_hot_tiles_spread_over_the_scouts(T, count, lo, hi):
+    """More hot tiles (over 2048 pairs) than segment_sort's scouts, so each scout opens several, and at
+    the 4K grid over more than one 8192-segment sweep: every one sorted, bit-identical, ranges exact."""
+    g = np.random.default_rng(T + count)
+    sizes = g.integers(lo, hi, count).tolist()
+    keys, vals = _many_hot_tiles(T, 1_000_000, sizes, count)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
+    ko, vo, r = primitives.sort_tile_pairs(u64(keys), u32(vals), T)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
+
+
+def test_one_workgroup_global_form_variant():
+    """The one-workgroup global form (four LSD passes through the alternate buffer) sorts tiles of
+    2049..8192 pairs in a build with HIDEGS_QUEUE_MIN=8192 (build.VARIANTS['gform']); the product build
+    sends them to the partition queue instead.  It is also the queue's fallback when its record table
+    or pool is full, so it stays tested."""
+    from hidegs_amd import _lib, build
+    var = _lib.load_library(build.variant_path("gform"))
+    T = 8160
+    g = np.random.default_rng(21)
+    sizes = [2049, 2050, 3000, 4095, 4096, 4097, 6000, 8191, 8192] + g.integers(2049, 8193, 60).tolist()
+    keys, vals = _many_hot_tiles(T, 600_000, sizes, 21)
+    keys[::13] = keys[7]  # ties across and inside tiles
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
+    rc, ko, vo, r = _variant_sort_tile_pairs(var, u64(keys), u32(vals), T)
+    assert rc == 0
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
+
+
 def test_queue_overflow_is_reported_not_silent():
     """A build whose partition queue holds 64 job slots (build.VARIANTS['qcap']) cannot queue a 300K-pair
     hot tile's jobs: the sort must report it -- through the sticky error word (hidegs_queue_error),
@@ -380,16 +440,10 @@ def test_queue_overflow_is_reported_not_silent():
     keys = np.concatenate([keys, hot])[g.permutation(500_000)]
     vals = np.arange(keys.size, dtype=np.uint32)
     kd, vd = u64(keys), u32(vals)
-    n = keys.size
-    dev = kd.device
-    stream = _lib.stream_handle(dev)
+    stream = _lib.stream_handle(kd.device)
 
     def run():
-        ko, vo = torch.empty_like(kd), torch.empty_like(vd)
-        rng = torch.empty((T, 2), dtype=torch.int32, device=dev)
-        tmp = torch.empty(int(var.hidegs_sort_pairs_u64_scratch_bytes(n)), dtype=torch.uint8, device=dev)
-        rc = var.hidegs_sort_tile_pairs(_lib.ptr(tmp), tmp.numel(), _lib.ptr(kd), _lib.ptr(ko), _lib.ptr(vd),
-                                        _lib.ptr(vo), n, T, _lib.ptr(rng), stream)
+        rc, _, vo, _ = _variant_sort_tile_pairs(var, kd, vd, T)
         return rc, vo
 
     flags = C.c_uint32(0)
