@@ -620,7 +620,12 @@ __device__ __forceinline__ void scatter_step(const uint64_t* sk, const uint32_t*
     for (int q = 0; q < kBigItems; q++) {
         if (ok[q]) {
             const uint32_t dd = digit_of(k[q], shift, mask);
+#ifdef HIDEGS_EXP_INORDER_SCATTER  // experiments only: input-order stores (wrong result; store-pattern A/B)
+            const uint32_t dst = base + w0 + q * kWave + lane;
+            (void)rank;
+#else
             const uint32_t dst = sh.run[dd] + sh.cnt[wave][dd] + rank[q];
+#endif
             if (dst >= lo && dst < hi) {
                 dk[dst] = k[q];
                 dv[dst] = v[q];
@@ -859,7 +864,8 @@ struct BigQueue {
 };
 
 #ifdef HIDEGS_QUEUE_TRACE  // experiments only: per-job timestamps (tools/queue_trace.py)
-__device__ unsigned long long g_qtrace[8192][4];  // (type | block << 8 | index << 32, claimed, started, ended)
+constexpr unsigned int kQTraceCap = 32768;
+__device__ unsigned long long g_qtrace[kQTraceCap][4];  // (type | block << 8 | index << 32, claimed, started, ended)
 __device__ unsigned int g_qtrace_n;
 #endif
 __device__ __forceinline__ uint32_t q_add(uint32_t* p, uint32_t v)
@@ -1788,7 +1794,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
 #ifdef HIDEGS_QUEUE_TRACE
         if (t == 0) {
             const unsigned int slot = atomicAdd(&g_qtrace_n, 1u);
-            if (slot < 8192) {
+            if (slot < kQTraceCap) {
                 const uint32_t last = (type == J_REDUCE || type == J_HIST || type == J_SCATTER) && s_flag ? 0x80u : 0u;
                 g_qtrace[slot][0] = (unsigned long long)(type | last | (blockIdx.x << 8)) | ((unsigned long long)t_index << 32);
                 g_qtrace[slot][1] = t_claim;

@@ -20,22 +20,31 @@ fn = L.hidegs_debug_queue_trace
 fn.restype = C.c_int
 fn.argtypes = [C.c_void_p, C.c_int]
 
-wl = synthetic.binning_workload(2_000_000, 1920, 1080, seed=0, device="cuda")
-buf = np.zeros((8192, 4), np.uint64)
-for hot in [int(a) for a in sys.argv[1:]] or [4096, 100_000]:
-    keys = wl.keys.clone()
-    idx = torch.randperm(keys.numel(), device="cuda")[:hot]
-    keys[idx] = (keys[idx] & 0xFFFFFFFF) | (4000 << 32)
+CAP = 32768
+buf = np.zeros((CAP, 4), np.uint64)
+cam = synthetic.d2_camera(1920, 1080)
+for spec in sys.argv[1:] or ["4096", "100000", "skew:0.15:0.1", "skew:0.5:0.02"]:
+    if spec.startswith("skew:"):  # a D2 view with a fraction of the Gaussians in a disc (tools/skew_time.py)
+        frac, rad = (float(x) for x in spec.split(":")[1:])
+        wl = synthetic.d2_binning_workload(synthetic.d2_scene(2_000_000, cam, seed=1000, cluster=(frac, rad)), cam,
+                                           device="cuda")
+        keys, hot = wl.keys, spec
+    else:  # `hot` pairs of round 3's synthetic keys moved into tile 4000
+        wl = synthetic.binning_workload(2_000_000, 1920, 1080, seed=0, device="cuda")
+        hot = int(spec)
+        keys = wl.keys.clone()
+        idx = torch.randperm(keys.numel(), device="cuda")[:hot]
+        keys[idx] = (keys[idx] & 0xFFFFFFFF) | (4000 << 32)
     primitives.sort_tile_pairs(keys, wl.values, wl.num_tiles)
     torch.cuda.synchronize()
-    fn(buf.ctypes.data, 8192)  # drop the warm-up's trace
+    fn(buf.ctypes.data, CAP)  # drop the warm-up's trace
     primitives.sort_tile_pairs(keys, wl.values, wl.num_tiles)
-    n = fn(buf.ctypes.data, 8192)
+    n = fn(buf.ctypes.data, CAP)
     tr = buf[:n].copy()
     t0 = tr[:, 1].min()
     rel = (tr[:, 1:].astype(np.int64) - int(t0)) / 100.0
     order = np.argsort(rel[:, 1])
-    print(f"hot tile {hot} pairs: {n} jobs, last end {rel[:, 2].max():.1f} us")
+    print(f"hot tile {hot}: {n} jobs, last end {rel[:, 2].max():.1f} us")
     kinds = {}
     for j in order:
         ty = int(tr[j, 0] & 0x7F)
