@@ -29,7 +29,8 @@ on this path is measured for real, at the configuration the metric is quoted on 
               wave-instructions per second from the committed PMC summary, against the chip's).
   config5_scale = the binning step and distCUDA2 at config 5's size (10M Gaussians, 4K frame).
   exchange  = the view-DP exchange of 2M x 59 fp32 leaf gradients + stats over RCCL (no
-              collective at N = 1), HIP-event timed; algbw and ring busbw.
+              collective at N = 1), HIP-event timed; algbw and ring busbw.  exchange_bf16: the same
+              with the bf16 wire (all-to-all + fp32 sums + all-gather; view_dp.py, transport="bf16").
   exchange_and_step = the exchange followed by the masked step, sequential and overlapped.
   masked Adam = the fused row-masked optimizer step at 2M Gaussians (59 fp32 each), 90% visible.
   cpu_baseline = on rank 0 at N = 1, every CPU leg on the same `cores` threads (the box's CPU
@@ -411,18 +412,22 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
     arena.flat.normal_(generator=g)
     norm = torch.rand(N, 1, device=dev, generator=g)
     radii = torch.rand(N, device=dev, generator=g)
-    ex = ViewDPExchange()
     reps = 20 if gpu else 3
-    ex_ms, ex_wall = timed(lambda: ex.exchange(arena, visible, max_stats=[norm, radii]), reps, 2)
-    nbytes = ex.last.reduced_bytes
-    algbw = nbytes / (ex_ms * 1e-3) / 1e9 if nbytes else None
-    line["exchange"] = {"ms_per_step": round(ex_ms, 3), "wall_ms_per_step": round(ex_wall, 3), "world": world,
-                        "timing": "HIP events on the compute stream (it waits for every RCCL bucket)" if gpu
-                        else "wall clock (gloo, CPU)",
-                        "grad_bytes_per_rank": nbytes, "algbw_GBps": algbw,
-                        "busbw_GBps": None if algbw is None else algbw * 2 * (world - 1) / world,
-                        "collectives_per_step": ex.last.collectives, "compacted": ex.last.compacted,
-                        "union_rows": ex.last.union_rows}
+    for transport in ("fp32", "bf16"):
+        ex = ViewDPExchange(transport=transport)
+        ex_ms, ex_wall = timed(lambda: ex.exchange(arena, visible, max_stats=[norm, radii]), reps, 2)
+        nbytes = ex.last.reduced_bytes
+        algbw = nbytes / (ex_ms * 1e-3) / 1e9 if nbytes else None
+        line["exchange" if transport == "fp32" else "exchange_bf16"] = {
+            "ms_per_step": round(ex_ms, 3), "wall_ms_per_step": round(ex_wall, 3), "world": world,
+            "transport": transport,
+            "timing": "HIP events on the compute stream (it waits for every RCCL bucket)" if gpu
+            else "wall clock (gloo, CPU)",
+            "grad_bytes_per_rank": nbytes, "wire_bytes_per_rank": ex.last.wire_bytes,
+            "algbw_GBps": algbw,  # fp32 gradient bytes made consistent per second
+            "busbw_GBps": None if algbw is None else algbw * 2 * (world - 1) / world,
+            "collectives_per_step": ex.last.collectives, "compacted": ex.last.compacted,
+            "union_rows": ex.last.union_rows}
     st = ctx.get("adam_state")
     if st is not None:
         prm, opt, vis, g2 = st
@@ -439,8 +444,10 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
 
         seq_ms, _ = timed(seq_step, 10, 2)
         fused_ms, _ = timed(lambda: ex2.exchange_and_step(arena2, vis, opt, prm, max_stats=[norm2]), 10, 2)
+        ex3 = ViewDPExchange(transport="bf16")
+        bf16_ms, _ = timed(lambda: ex3.exchange_and_step(arena2, vis, opt, prm, max_stats=[norm2]), 10, 2)
         line["exchange_and_step"] = {"world": world, "sequential_ms": round(seq_ms, 3),
-                                     "overlapped_ms": round(fused_ms, 3),
+                                     "overlapped_ms": round(fused_ms, 3), "overlapped_bf16_ms": round(bf16_ms, 3),
                                      "collectives": ex2.last.collectives, "union_rows": ex2.last.union_rows}
 
 

@@ -31,6 +31,15 @@ the CPU tests.  Bitwise OR is formed from an all-gather of packed masks (RCCL ha
 bitwise reduction), which also yields the per-Gaussian view count.  A one-rank group has
 nothing to exchange and issues no collective.
 
+Transport (`transport=`): "fp32" (default) all-reduces the fp32 gradients as they are.  "bf16" halves
+the bytes on the wire with the sum still formed in fp32: each bucket is rounded to bf16 (nearest-even)
+and split into `world` chunks; one all-to-all hands chunk c of every rank to rank c, which adds them in
+fp32 in rank order (0, 1, ...) and rounds the sum to bf16 once; one all-gather returns every chunk's
+sum to every rank.  The result is each element's bf16(sum_r bf16(g_r)) -- within ~2^-8 relative of the
+fp32 sum per input plus one output rounding, identical on every rank (each chunk is summed by exactly
+one rank, in a fixed order), so the replicas stay bit-identical.  It is a semantic change (SURVEY §8(e)
+E2 item 3: "bf16 transport, behind a parity flag"); the default stays fp32.
+
 `exchange_and_step` fuses the exchange with the masked optimizer step that follows it: each
 dense bucket's rows are updated as soon as that bucket's all-reduce lands, while the later
 buckets are still reducing (SURVEY §8(e) E2's overlap; the backward that would also overlap it is
@@ -125,9 +134,62 @@ class GradArena:
 @dataclass
 class ExchangeStats:
     union_rows: int = 0
-    reduced_bytes: int = 0
+    reduced_bytes: int = 0  # fp32 gradient bytes summed over ranks (per rank)
+    wire_bytes: int = 0     # bytes this rank handed to the collectives for them (bf16: half)
     collectives: int = 0
     compacted: bool = False
+
+
+TRANSPORTS = ("fp32", "bf16")
+
+
+class _Bucket:
+    """One gradient bucket's SUM over the group, in three steps so that several buckets can be in
+    flight: start() issues the first collective, mid() the second (bf16 only: the fp32 sum of this
+    rank's chunk between the two), finish() waits and leaves the summed values in `view` (fp32)."""
+
+    def __init__(self, view: torch.Tensor, group, transport: str, world: int, rank: int):
+        self.view, self.group, self.transport, self.world, self.rank = view, group, transport, world, rank
+        self.work = None
+
+    def start(self) -> int:
+        if self.transport == "fp32":
+            self.work = dist.all_reduce(self.view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            return 1
+        n, w = self.view.numel(), self.world
+        self.chunk = -(-n // (8 * w)) * 8  # 16-byte aligned chunks, one per rank
+        send = torch.zeros(self.chunk * w, dtype=torch.bfloat16, device=self.view.device)
+        send[:n].copy_(self.view.reshape(-1))  # round to nearest even
+        self.recv = torch.empty_like(send)
+        # bf16 moved as bytes: the collective only moves them (gloo has no 16-bit all-to-all)
+        self.work = dist.all_to_all_single(self.recv.view(torch.uint8), send.view(torch.uint8), group=self.group,
+                                           async_op=True)
+        self.send = send
+        return 1
+
+    def mid(self) -> int:
+        if self.transport == "fp32":
+            return 0
+        self.work.wait()
+        parts = self.recv.view(self.world, self.chunk)
+        acc = parts[0].to(torch.float32)
+        for r in range(1, self.world):  # fp32, rank order: the same sum on whichever rank owns the chunk
+            acc += parts[r].to(torch.float32)
+        mine = acc.to(torch.bfloat16)
+        self.gathered = torch.empty_like(self.send)
+        self.work = dist.all_gather_into_tensor(self.gathered.view(torch.uint8), mine.view(torch.uint8),
+                                                group=self.group, async_op=True)
+        return 1
+
+    def finish(self) -> None:
+        self.work.wait()
+        if self.transport == "bf16":
+            self.view.reshape(-1).copy_(self.gathered[:self.view.numel()])
+            self.send = self.recv = self.gathered = None
+
+    @property
+    def wire_bytes(self) -> int:
+        return self.view.numel() * (4 if self.transport == "fp32" else 2)
 
 
 @dataclass
@@ -140,11 +202,14 @@ class ViewDPExchange:
     """One exchange step per training iteration of view-data-parallel rendering."""
 
     def __init__(self, group: Optional[dist.ProcessGroup] = None, bucket_bytes: int = 64 << 20,
-                 compact_below: float = 0.75, debug: bool = False):
+                 compact_below: float = 0.75, debug: bool = False, transport: str = "fp32"):
         if bucket_bytes < 4:
             raise ValueError("bucket_bytes must hold at least one fp32 value")
         if not 0.0 <= compact_below <= 1.0:
             raise ValueError("compact_below is a fraction of rows in [0, 1]")
+        if transport not in TRANSPORTS:
+            raise ValueError(f"transport must be one of {TRANSPORTS}")
+        self.transport = transport
         self.group = group
         self.bucket_bytes = int(bucket_bytes)
         self.compact_below = float(compact_below)
@@ -168,16 +233,31 @@ class ViewDPExchange:
         return count > 0, count.to(torch.float32).unsqueeze(1)
 
     # ---- leaf gradients -----------------------------------------------------------
+    def _bucket(self, view: torch.Tensor) -> _Bucket:
+        return _Bucket(view, self.group, self.transport, dist.get_world_size(self.group), dist.get_rank(self.group))
+
+    def _run_buckets(self, buckets: List[_Bucket], after=None) -> None:
+        """Every bucket's first collective issued at once, then per bucket in order: its second
+        collective (bf16) issued one bucket ahead, its wait, and `after(i)` (e.g. that bucket's rows'
+        optimizer update) while the later buckets are still on the wire."""
+        for b in buckets:
+            self.last.collectives += b.start()
+            self.last.wire_bytes += b.wire_bytes
+            self.last.reduced_bytes += b.view.numel() * 4
+        if buckets:
+            self.last.collectives += buckets[0].mid()
+        for i, b in enumerate(buckets):
+            if i + 1 < len(buckets):
+                self.last.collectives += buckets[i + 1].mid()
+            b.finish()
+            if after is not None:
+                after(i)
+
     def _all_reduce_buckets(self, flat: torch.Tensor) -> None:
         if dist.get_world_size(self.group) == 1:  # the sum over one rank is the tensor itself
             return
         per = max(1, self.bucket_bytes // flat.element_size())
-        works = [dist.all_reduce(flat[s:s + per], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-                 for s in range(0, flat.numel(), per)]
-        for w in works:
-            w.wait()
-        self.last.collectives += len(works)
-        self.last.reduced_bytes += flat.numel() * flat.element_size()
+        self._run_buckets([self._bucket(flat[s:s + per]) for s in range(0, flat.numel(), per)])
 
     def sum_gradients(self, grads: Union[GradArena, Iterable[torch.Tensor]],
                       union: Optional[torch.Tensor] = None) -> None:
@@ -320,21 +400,25 @@ class ViewDPExchange:
             optimizer.begin_step(union).run()  # counters advance only once the gradients are summed
         else:
             self.last.union_rows = nu
-            works = []
+            spans, buckets = [], []
             for name, w in arena.widths.items():
                 rows = max(4, (self.bucket_bytes // (4 * w)) // 4 * 4)  # 4-row multiples keep 16-byte alignment
                 view = arena.views[name]
                 for r0 in range(0, n, rows):
                     r1 = min(n, r0 + rows)
-                    works.append((dist.all_reduce(view[r0:r1], op=dist.ReduceOp.SUM, group=self.group,
-                                                  async_op=True), name, r0, r1))
-            self.last.collectives += len(works)
-            self.last.reduced_bytes += arena.flat.numel() * arena.flat.element_size()
-            # the step counters advance once every collective has been issued
-            plan = optimizer.begin_step(union)
-            for work, name, r0, r1 in works:
-                work.wait()  # the current stream waits for this bucket; later buckets keep reducing
-                plan.run_rows(params[name], r0, r1)
+                    spans.append((name, r0, r1))
+                    buckets.append(self._bucket(view[r0:r1]))
+            plans = []
+
+            def step_rows(i):
+                # the step counters advance once every first collective has been issued
+                if not plans:
+                    plans.append(optimizer.begin_step(union))
+                name, r0, r1 = spans[i]
+                plans[0].run_rows(params[name], r0, r1)  # later buckets keep reducing meanwhile
+
+            self._run_buckets(buckets, after=step_rows)
+            plan = plans[0] if plans else optimizer.begin_step(union)
             # parameters the plan steps that are not arena fields (their gradients were not exchanged
             # here): stepped whole, as optimizer.step(union) would
             plan.run_except([params[k] for k in arena.widths])

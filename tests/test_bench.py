@@ -24,4 +24,6 @@ def test_bench_launches_its_own_ranks_gloo():
     ex = rec["exchange"]
     assert ex["world"] == 2 and ex["collectives_per_step"] > 0
     assert ex["grad_bytes_per_rank"] == 20000 * 59 * 4 and ex["algbw_GBps"] > 0
+    bx = rec["exchange_bf16"]
+    assert bx["wire_bytes_per_rank"] * 2 == bx["grad_bytes_per_rank"] and bx["collectives_per_step"] > 0
     assert rec["value"] is None  # the headline stays unmeasured

@@ -202,7 +202,7 @@ class RecordingOptimizer:
         return self.plan
 
 
-def worker_step(rank, world, port, compact_below, bucket_bytes, q):
+def worker_step(rank, world, port, compact_below, bucket_bytes, q, transport="fp32"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -215,10 +215,13 @@ def worker_step(rank, world, port, compact_below, bucket_bytes, q):
             arena[k].copy_(v)
         plan = RecordingPlan(arena, {id(p): k for k, p in params.items()})
         opt = RecordingOptimizer(plan)
-        ex = ViewDPExchange(bucket_bytes=bucket_bytes, compact_below=compact_below)
+        ex = ViewDPExchange(bucket_bytes=bucket_bytes, compact_below=compact_below, transport=transport)
         res = ex.exchange_and_step(arena, visible, opt, params, max_stats=[norm])
         all_in = [rank_inputs(r, 0) for r in range(world)]
-        exp = {k: sum(a[1][k] for a in all_in) for k in LEAF_WIDTHS}
+        if transport == "bf16" and world > 1:
+            exp = {k: bf16_sum([a[1][k] for a in all_in]) for k in LEAF_WIDTHS}
+        else:
+            exp = {k: sum(a[1][k] for a in all_in) for k in LEAF_WIDTHS}
         exp_union = torch.zeros(N, dtype=torch.bool)
         for a in all_in:
             exp_union |= a[0]
@@ -245,11 +248,11 @@ def worker_step(rank, world, port, compact_below, bucket_bytes, q):
         dist.destroy_process_group()
 
 
-def run_step(world, compact_below, bucket_bytes):
+def run_step(world, compact_below, bucket_bytes, transport="fp32"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker_step, args=(r, world, port, compact_below, bucket_bytes, q))
+    procs = [ctx.Process(target=worker_step, args=(r, world, port, compact_below, bucket_bytes, q, transport))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -259,17 +262,86 @@ def run_step(world, compact_below, bucket_bytes):
     return q.get(timeout=10)
 
 
-@pytest.mark.parametrize("world,compact_below,bucket_bytes,mode", [
-    (2, 0.0, 4096, "rows"),       # dense: per-bucket steps overlapped with the later buckets' reduces
-    (3, 0.0, 1 << 20, "rows"),
-    (2, 1.0, 4096, "whole"),      # compacted: reduce, then one step
-    (1, 0.0, 4096, "whole"),      # one rank: no collective at all
+@pytest.mark.parametrize("world,compact_below,bucket_bytes,mode,transport", [
+    (2, 0.0, 4096, "rows", "fp32"),       # dense: per-bucket steps overlapped with the later buckets' reduces
+    (3, 0.0, 1 << 20, "rows", "fp32"),
+    (2, 1.0, 4096, "whole", "fp32"),      # compacted: reduce, then one step
+    (1, 0.0, 4096, "whole", "fp32"),      # one rank: no collective at all
+    (2, 0.0, 4096, "rows", "bf16"),       # bf16 wire: all-to-all + all-gather per bucket, pipelined
+    (3, 0.0, 1 << 20, "rows", "bf16"),
+    (3, 1.0, 4096, "whole", "bf16"),
 ])
-def test_exchange_and_step_steps_each_row_once_after_its_reduction(world, compact_below, bucket_bytes, mode):
-    ok, got_mode, collectives = run_step(world, compact_below, bucket_bytes)
+def test_exchange_and_step_steps_each_row_once_after_its_reduction(world, compact_below, bucket_bytes, mode, transport):
+    ok, got_mode, collectives = run_step(world, compact_below, bucket_bytes, transport)
     assert ok and got_mode == mode
     if world == 1:
         assert collectives == 0
+
+
+def bf16_sum(parts):
+    """The bf16 transport's definition: every rank's values rounded to bf16 (nearest even), added in
+    fp32 in rank order, the sum rounded to bf16 once (returned as fp32)."""
+    acc = parts[0].to(torch.bfloat16).to(torch.float32)
+    for x in parts[1:]:
+        acc = acc + x.to(torch.bfloat16).to(torch.float32)
+    return acc.to(torch.bfloat16).to(torch.float32)
+
+
+def worker_bf16(rank, world, port, compact_below, bucket_bytes, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ex = ViewDPExchange(bucket_bytes=bucket_bytes, compact_below=compact_below, transport="bf16")
+        ok, rel = True, 0.0
+        for step in range(2):
+            visible, grads, norm, _ = rank_inputs(rank, step)
+            arena = GradArena(N)
+            for k, v in grads.items():
+                arena[k].copy_(v)
+            ex.exchange(arena, visible, max_stats=[norm])
+            all_in = [rank_inputs(r, step) for r in range(world)]
+            for k in LEAF_WIDTHS:
+                parts = [a[1][k] for a in all_in]
+                ok = ok and torch.equal(arena[k], bf16_sum(parts))  # the definition, bit for bit
+                exact = sum(p.double() for p in parts)
+                scale = sum(p.double().abs() for p in parts)
+                rel = max(rel, float(((arena[k].double() - exact).abs() / scale.clamp(min=1e-30)).max()))
+            # replicas identical: every rank's summed arena, bit for bit
+            got = [torch.empty_like(arena.flat) for _ in range(world)]
+            dist.all_gather(got, arena.flat)
+            ok = ok and all(torch.equal(g.view(torch.int32), got[0].view(torch.int32)) for g in got)
+        if rank == 0:
+            q.put((ok, rel, ex.last.wire_bytes, ex.last.reduced_bytes, ex.last.compacted))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,compact_below,bucket_bytes", [(2, 0.0, 64 << 20), (3, 0.0, 4096), (3, 1.0, 1000),
+                                                              (4, 0.0, 10000)])
+def test_bf16_transport_is_its_definition_and_identical_on_every_rank(world, compact_below, bucket_bytes):
+    """transport="bf16": half the wire bytes, the sum formed in fp32 by the chunk's owner; the result
+    equals bf16(sum_r bf16(g_r)) exactly and is the same on every rank; within 2^-7 of the exact sum
+    relative to sum_r |g_r| (two bf16 roundings of relative 2^-9 each, plus fp32 adds)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker_bf16, args=(r, world, port, compact_below, bucket_bytes, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    ok, rel, wire, reduced, compacted = q.get(timeout=10)
+    assert ok, "bf16 exchange differs from its definition or between ranks"
+    assert rel <= 2.0 ** -7, rel
+    assert wire * 2 == reduced and compacted == (compact_below == 1.0)
+
+
+def test_transport_is_checked():
+    with pytest.raises(ValueError, match="transport"):
+        ViewDPExchange(transport="fp16")
 
 
 def test_detached_grad_is_refused():
