@@ -89,9 +89,15 @@ __device__ __forceinline__ float box_box_lb(const Box& b, float4 qlo, float4 qhi
 // Every value here is a non-negative float (a sum of squares, FLT_MAX or +inf), whose bit
 // patterns order like unsigned integers: the min/max network runs on the bits, which spares the
 // NaN-quieting canonicalisation that fminf/fmaxf of loop-carried values costs on gfx950.
+// No NaN test is needed (HIDEGS_KNN_NAN_CHECK=1 restores it for A/B): the three best only decrease
+// from FLT_MAX, and every NaN pattern -- and +inf -- is above FLT_MAX as an unsigned integer, so such a
+// d leaves them unchanged exactly as the reference's `dist < best` (false for NaN and inf) does.
+#ifndef HIDEGS_KNN_NAN_CHECK
+#define HIDEGS_KNN_NAN_CHECK 0
+#endif
 __device__ __forceinline__ void kbest(float d, float& b0, float& b1, float& b2)
 {
-    const uint32_t x = (d == d) ? __float_as_uint(d) : __float_as_uint(FLT_MAX);
+    const uint32_t x = (!HIDEGS_KNN_NAN_CHECK || d == d) ? __float_as_uint(d) : __float_as_uint(FLT_MAX);
     const uint32_t c0 = __float_as_uint(b0), c1 = __float_as_uint(b1), c2 = __float_as_uint(b2);
     const uint32_t t0 = min(c0, x), u0 = max(c0, x);
     const uint32_t t1 = min(c1, u0), u1 = max(c1, u0);
