@@ -342,6 +342,10 @@ constexpr int kBailout = HIDEGS_KNN_BAILOUT;  // candidate leaves after which a 
 #ifndef HIDEGS_KNN_SEED_NEIGHBORS
 #define HIDEGS_KNN_SEED_NEIGHBORS 1  // 0: seed from the own leaf only (A/B builds)
 #endif
+#ifndef HIDEGS_KNN_SCALAR_SUBS
+#define HIDEGS_KNN_SCALAR_SUBS 1  // sub-boxes by scalar loads (0: vector loads + readlanes): 893 -> 840 us frustum,
+                                  // 848 -> 787 uniform, 448 -> 492 plane (2M points)
+#endif
 #ifndef HIDEGS_KNN_POINT_FILTER
 #define HIDEGS_KNN_POINT_FILTER 1  // 0: evaluate whole passing sub-boxes (A/B builds, tools/build_variant.py)
 #endif
@@ -490,12 +494,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_K
                     if (i0 + q >= cnt) break;
                     n_coarse++;
                     uint32_t smask4 = HIDEGS_KNN_SUBBOX_FILTER ? 0u : (1u << kSub) - 1u;
+#if HIDEGS_KNN_SCALAR_SUBS
+                    // the leaf's sub-boxes by scalar loads (the leaf index is wave-uniform): no readlanes
+                    const Box* sbp = subs + (size_t)__builtin_amdgcn_readfirstlane(Cb[q]) * kSub;
+#endif
 #pragma unroll
                     for (int j = 0; j < kSub && HIDEGS_KNN_SUBBOX_FILTER; j++) {
+#if HIDEGS_KNN_SCALAR_SUBS
+                        const Box sb = sbp[j];
+#else
                         const Box sb{make_float4(uniform_lane(bx[q].x, 2 * j), uniform_lane(bx[q].y, 2 * j),
                                                  uniform_lane(bx[q].z, 2 * j), 0.f),
                                      make_float4(uniform_lane(bx[q].x, 2 * j + 1), uniform_lane(bx[q].y, 2 * j + 1),
                                                  uniform_lane(bx[q].z, 2 * j + 1), 0.f)};
+#endif
                         if (__ballot(active && box_point_lb(sb, p) <= b2)) smask4 |= 1u << j;
                     }
                     const int nc = min(kLeaf, P - Cb[q] * kLeaf);
