@@ -630,10 +630,12 @@ __device__ __forceinline__ void scatter_step(const uint64_t* sk, const uint32_t*
                 dk[dst] = k[q];
                 dv[dst] = v[q];
             }
+#ifndef HIDEGS_EXP_NO_TRACK  // experiments only: no per-digit AND / OR (wrong next-level digits; cost A/B)
             if (Track) {
                 atomicAnd(&sh.aux[0][dd], (uint32_t)k[q]);
                 atomicOr(&sh.aux[1][dd], (uint32_t)k[q]);
             }
+#endif
         }
     }
     __syncthreads();
@@ -836,8 +838,15 @@ constexpr int kQueueBlocks = HIDEGS_QUEUE_BLOCKS;
                               // every tile over kSegCap goes to the queue; tools/skew_time.py A/B in DESIGN.md)
 #endif
 constexpr int kQueueMin = HIDEGS_QUEUE_MIN;
+#ifndef HIDEGS_WIDE_CAP
+#define HIDEGS_WIDE_CAP 12288  // segments up to this many pairs: one WIDE job (LDS sort by one worker)
+#endif
+constexpr int kWideCap = HIDEGS_WIDE_CAP;
+#ifndef HIDEGS_WIDE_SCOUTS
+#define HIDEGS_WIDE_SCOUTS 0  // 1: scouts hand hot tiles of <= kWideCap pairs to the queue as WIDE jobs (slower: DESIGN.md)
+#endif
 constexpr uint32_t kMaxPolls = 1u << 22;
-enum : uint32_t { J_EXIT = 0, J_SMALL, J_COPY, J_REDUCE, J_HIST, J_SCATTER, J_GLOBAL };
+enum : uint32_t { J_EXIT = 0, J_SMALL, J_COPY, J_REDUCE, J_HIST, J_SCATTER, J_GLOBAL, J_WIDE };
 enum : int { Q_HEAD, Q_RESERVE, Q_DONE, Q_NREC, Q_POOL, Q_ERROR, Q_COUNTERS = 8 };
 constexpr int kCtlStride = 32;  // one 128-byte line per counter: polls of one do not queue behind another's atomics
 constexpr int Q_WORDS = Q_COUNTERS * kCtlStride;
@@ -867,6 +876,12 @@ struct BigQueue {
 constexpr unsigned int kQTraceCap = 32768;
 __device__ unsigned long long g_qtrace[kQTraceCap][4];  // (type | block << 8 | index << 32, claimed, started, ended)
 __device__ unsigned int g_qtrace_n;
+constexpr int kWTraceCap = 4096;
+__device__ unsigned long long g_wtrace[kWTraceCap][9];  // WIDE jobs: m, then 8 phase timestamps
+__device__ unsigned int g_wtrace_n;
+#define WSTAMP(k) do { if (threadIdx.x == 0 && wslot < kWTraceCap) g_wtrace[wslot][1 + (k)] = wall_clock64(); } while (0)
+#else
+#define WSTAMP(k) do { } while (0)
 #endif
 __device__ __forceinline__ uint32_t q_add(uint32_t* p, uint32_t v)
 {
@@ -1116,7 +1131,8 @@ __device__ __forceinline__ void cut_pieces(const BigQueue& q, EmitShared& e, Big
         uint4 run = make_uint4(0u, 0u, 0u, 0u);
         if (boundary) {
             if (n_d > (uint32_t)kSegCap)
-                run = record_run(q, begin + s_d, n_d, dst, diff_d);
+                run = n_d <= (uint32_t)kWideCap ? make_uint4(J_WIDE | (dst << 8), begin + s_d, n_d, 1u)
+                                                : record_run(q, begin + s_d, n_d, dst, diff_d);
             else if (next - s_d > 1u || dst)
                 run = make_uint4(J_SMALL | (dst << 8), begin + s_d, next - s_d, 1u);
         }
@@ -1134,6 +1150,286 @@ __device__ __forceinline__ void cut_pieces(const BigQueue& q, EmitShared& e, Big
     }
 }
 
+// A WIDE job: one segment of kSegCap < m <= kWideCap pairs sorted whole by ONE queue worker in LDS
+// (big_segment_kernel runs at one workgroup per CU, so it can hold 152 KB): the hot tiles of a skewed
+// view and the level-1 digits of a very hot one, each in one job instead of a record's chain of
+// REDUCE / HIST / SCATTER hand-offs and pieces (tools/skew_time.py: DESIGN.md "Skewed views").
+#ifndef HIDEGS_WIDE_ROUNDS
+#define HIDEGS_WIDE_ROUNDS 4  // 64-item rounds a wave ranks at once
+#endif
+constexpr int kWideRounds = HIDEGS_WIDE_ROUNDS;
+constexpr int kWideBatch = 8;  // global loads in flight per thread in the load and gather loops
+constexpr int kWideIndexBits = 14;
+#ifndef HIDEGS_WIDE_ILP
+#define HIDEGS_WIDE_ILP 4
+#endif
+constexpr int kWideIlp = HIDEGS_WIDE_ILP;  // items per thread in flight in the bucket form's LDS phases
+#ifndef HIDEGS_WIDE_MAX_BUCKET
+#define HIDEGS_WIDE_MAX_BUCKET 128  // a fuller bucket sends the WIDE segment to the LSD passes
+#endif
+constexpr int kWideMaxBucket = HIDEGS_WIDE_MAX_BUCKET;
+struct WideShared {
+    uint32_t k[2][kWideCap];  // low key halves
+    uint16_t i[2][kWideCap];  // index in the segment
+    uint32_t cnt[kWavesPerBlock][kRadix];
+    uint32_t wave[kWavesPerBlock];
+    uint32_t red[2][kWavesPerBlock];
+};
+static_assert(kWideCap <= (1 << kWideIndexBits) && kWideCap % kBlock == 0, "WIDE segment indices are u16 / 14 bits");
+static_assert(2 * kBuckets * sizeof(uint32_t) <= sizeof(uint16_t) * kWideCap, "bucket counters fit in i[0]");
+
+// Pairs [begin, begin + m) of (src ? alt : keys) sorted stably by their low 32 key bits into
+// keys / vals (m <= kWideCap).  The low halves and indices are sorted in LDS by stable 8-bit LSD
+// passes over the bits that vary (per pass: per-wave digit counts, their scan, then each wave ranks
+// its contiguous share in input order with wave_rank); the pairs are then gathered by index from alt
+// (src 0: copied there first, so keys can be written in place).
+__device__ __forceinline__ void wide_sort(uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                          uint64_t* __restrict__ alt_k, uint32_t* __restrict__ alt_v,
+                                          const uint32_t begin, const uint32_t m, const uint32_t src, WideShared& w)
+{
+    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
+    const uint64_t* sk = src ? alt_k : keys;
+#ifdef HIDEGS_QUEUE_TRACE
+    __shared__ unsigned int s_wslot;
+    if (t == 0) {
+        s_wslot = atomicAdd(&g_wtrace_n, 1u);
+        if (s_wslot < kWTraceCap) g_wtrace[s_wslot][0] = m;
+    }
+    __syncthreads();
+    const unsigned int wslot = s_wslot;
+#endif
+    WSTAMP(0);
+    uint32_t a = 0xffffffffu, o = 0u;
+    for (uint32_t i0 = 0; i0 < m; i0 += kBlock * kWideBatch) {  // kWideBatch loads in flight per thread
+        uint64_t kk[kWideBatch];
+        uint32_t vv[kWideBatch];
+#pragma unroll
+        for (int u = 0; u < kWideBatch; u++) {
+            const uint32_t i = i0 + u * kBlock + t;
+            if (i < m) {
+                kk[u] = sk[begin + i];
+                if (!src) vv[u] = vals[begin + i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kWideBatch; u++) {
+            const uint32_t i = i0 + u * kBlock + t;
+            if (i < m) {
+                const uint32_t lo = (uint32_t)kk[u];
+                w.k[0][i] = lo;
+                w.i[0][i] = (uint16_t)i;
+                a &= lo;
+                o |= lo;
+                if (!src) {
+                    alt_k[begin + i] = kk[u];
+                    alt_v[begin + i] = vv[u];
+                }
+            }
+        }
+    }
+    wave_and_or(a, o);
+    if (lane == 0) {
+        w.red[0][wave] = a;
+        w.red[1][wave] = o;
+    }
+    __syncthreads();
+    a = 0xffffffffu;
+    o = 0u;
+#pragma unroll
+    for (int ww = 0; ww < kWavesPerBlock; ww++) {
+        a &= w.red[0][ww];
+        o |= w.red[1][ww];
+    }
+    const uint32_t diff = a ^ o;  // block-uniform
+    WSTAMP(1);
+    int cur = 0;
+    // Bucket form (as segment_sort's): the top kBucketBits varying bits pick a bucket, and an item's
+    // place in its bucket is its exact rank by (key bits below the bucket digit || index), so equal
+    // keys keep their input order.  Its start / fill counters borrow the storage of i[0].
+    const int top = diff ? 31 - __builtin_clz(diff) : 0;
+    const int dbits = top + 1 < kBucketBits ? top + 1 : kBucketBits;
+    const int bshift = top + 1 - dbits;
+    bool lsd = diff != 0u;
+    if (diff && bshift + kWideIndexBits <= 32) {  // block-uniform
+        const uint32_t dmask = (1u << dbits) - 1u;
+        const uint32_t lowmask = (uint32_t)((1ull << bshift) - 1ull);
+        uint32_t* start = reinterpret_cast<uint32_t*>(&w.i[0][0]);
+        uint32_t* fill = start + kBuckets;
+        for (int b = t; b < kBuckets; b += kBlock) fill[b] = 0u;
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < m; i0 += kWideIlp * kBlock) {  // kWideIlp independent items per thread
+            uint32_t x[kWideIlp];
+#pragma unroll
+            for (int u = 0; u < kWideIlp; u++) {
+                const uint32_t i = i0 + u * kBlock + t;
+                x[u] = i < m ? w.k[0][i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kWideIlp; u++)
+                if (i0 + u * kBlock + t < m) atomicAdd(&fill[(x[u] >> bshift) & dmask], 1u);
+        }
+        __syncthreads();
+        WSTAMP(2);
+        uint32_t c[kBuckets / kBlock], sum = 0, mx = 0;
+#pragma unroll
+        for (int j = 0; j < kBuckets / kBlock; j++) {
+            c[j] = fill[t * (kBuckets / kBlock) + j];
+            sum += c[j];
+            mx = c[j] > mx ? c[j] : mx;
+        }
+        uint32_t dummy;
+        uint32_t pre = block_exclusive_scan(sum, w.wave, &dummy);  // its barriers order the reads above
+#pragma unroll
+        for (int sft = 32; sft >= 1; sft >>= 1) {
+            const uint32_t y = __shfl_xor(mx, sft, kWave);
+            mx = y > mx ? y : mx;
+        }
+        if (lane == 0) w.red[0][wave] = mx;
+#pragma unroll
+        for (int j = 0; j < kBuckets / kBlock; j++) {
+            start[t * (kBuckets / kBlock) + j] = pre;
+            fill[t * (kBuckets / kBlock) + j] = pre;
+            pre += c[j];
+        }
+        __syncthreads();
+        uint32_t fullest = 0;
+#pragma unroll
+        for (int ww = 0; ww < kWavesPerBlock; ww++) fullest = w.red[0][ww] > fullest ? w.red[0][ww] : fullest;
+        WSTAMP(3);
+        if (fullest <= (uint32_t)kWideMaxBucket) {  // block-uniform
+            uint32_t* comb = w.k[1];
+            for (uint32_t i0 = 0; i0 < m; i0 += kWideIlp * kBlock) {
+                uint32_t x[kWideIlp], slot[kWideIlp];
+#pragma unroll
+                for (int u = 0; u < kWideIlp; u++) {
+                    const uint32_t i = i0 + u * kBlock + t;
+                    x[u] = i < m ? w.k[0][i] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < kWideIlp; u++)
+                    if (i0 + u * kBlock + t < m) slot[u] = atomicAdd(&fill[(x[u] >> bshift) & dmask], 1u);
+#pragma unroll
+                for (int u = 0; u < kWideIlp; u++) {
+                    const uint32_t i = i0 + u * kBlock + t;
+                    if (i < m) comb[slot[u]] = ((x[u] & lowmask) << kWideIndexBits) | i;
+                }
+            }
+            __syncthreads();
+            WSTAMP(4);
+            for (uint32_t i0 = 0; i0 < m; i0 += kWideIlp * kBlock) {
+                uint32_t me[kWideIlp], s0[kWideIlp], e0[kWideIlp], rank[kWideIlp];
+                uint32_t len = 0;
+#pragma unroll
+                for (int u = 0; u < kWideIlp; u++) {
+                    const uint32_t i = i0 + u * kBlock + t;
+                    const uint32_t x = i < m ? w.k[0][i] : 0u;
+                    const uint32_t bk = (x >> bshift) & dmask;
+                    me[u] = ((x & lowmask) << kWideIndexBits) | i;
+                    s0[u] = start[bk];
+                    e0[u] = i < m ? fill[bk] : s0[u];
+                    rank[u] = 0u;
+                    len = e0[u] - s0[u] > len ? e0[u] - s0[u] : len;
+                }
+                for (uint32_t j = 0; j < len; j++) {  // the kWideIlp bucket walks interleaved
+#pragma unroll
+                    for (int u = 0; u < kWideIlp; u++)
+                        if (s0[u] + j < e0[u]) rank[u] += comb[s0[u] + j] < me[u] ? 1u : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < kWideIlp; u++)
+                    if (i0 + u * kBlock + t < m) w.i[1][s0[u] + rank[u]] = (uint16_t)(i0 + u * kBlock + t);
+            }
+            __syncthreads();
+            WSTAMP(5);
+            cur = 1;
+            lsd = false;
+        } else {  // crowded buckets: the LSD passes below, whose i[0] the counters overwrote
+            for (uint32_t i = t; i < m; i += kBlock) w.i[0][i] = (uint16_t)i;
+            __syncthreads();
+        }
+    }
+    const uint32_t C = (m + kBlock - 1) / kBlock * kWave;  // each wave's contiguous share (64-item rounds)
+    const uint32_t w0 = wave * C, w1 = w0 + C < m ? w0 + C : m;
+    for (int shift = 0; shift < 32 && lsd; shift += kRadixBits) {
+        const uint32_t vary = (diff >> shift) & (kRadix - 1);
+        if (vary == 0) continue;  // digit constant over the segment (block-uniform)
+        for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&w.cnt[0][0])[i] = 0u;
+        __syncthreads();
+        for (uint32_t i0 = w0; i0 < w1; i0 += 4 * kWave) {
+            uint32_t x[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0 + u * kWave + lane;
+                x[u] = i < w1 ? w.k[cur][i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (i0 + u * kWave + lane < w1) atomicAdd(&w.cnt[wave][(x[u] >> shift) & (kRadix - 1)], 1u);
+        }
+        __syncthreads();
+        const uint32_t tot = digit_wave_prefix(w.cnt);  // cnt[ww][d]: digit d in waves before ww
+        uint32_t dummy;
+        const uint32_t start = block_exclusive_scan(tot, w.wave, &dummy);  // its barriers order the above
+#pragma unroll
+        for (int ww = 0; ww < kWavesPerBlock; ww++) w.cnt[ww][t] += start;  // thread t owns digit t
+        __syncthreads();
+        for (uint32_t r0 = w0; r0 < w1; r0 += kWideRounds * kWave) {  // wave-uniform
+            uint32_t kk[kWideRounds], id[kWideRounds], rank[kWideRounds];
+            bool ok[kWideRounds];
+#pragma unroll
+            for (int q = 0; q < kWideRounds; q++) {
+                const uint32_t i = r0 + q * kWave + lane;
+                ok[q] = i < w1;
+                kk[q] = ok[q] ? w.k[cur][i] : 0u;
+                id[q] = ok[q] ? w.i[cur][i] : 0u;
+            }
+            // cnt starts at each digit's first position for this wave: rank = the item's position
+            wave_rank<uint32_t, kWideRounds>(kk, ok, shift, kRadix - 1, w.cnt[wave], rank, vary);
+#pragma unroll
+            for (int q = 0; q < kWideRounds; q++) {
+                if (ok[q]) {
+                    w.k[cur ^ 1][rank[q]] = kk[q];
+                    w.i[cur ^ 1][rank[q]] = (uint16_t)id[q];
+                }
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    WSTAMP(6);
+    if (!diff && !src) return;  // equal low keys, in place: the input order is the stable order
+    for (uint32_t j0 = 0; j0 < m; j0 += kBlock * kWideBatch) {
+        uint32_t ii[kWideBatch];
+        uint64_t kk[kWideBatch];
+        uint32_t vv[kWideBatch];
+#pragma unroll
+        for (int u = 0; u < kWideBatch; u++) {
+            const uint32_t j = j0 + u * kBlock + t;
+            ii[u] = j < m ? w.i[cur][j] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kWideBatch; u++) {
+            if (j0 + u * kBlock + t < m) {
+                kk[u] = alt_k[begin + ii[u]];
+                vv[u] = alt_v[begin + ii[u]];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kWideBatch; u++) {
+            const uint32_t j = j0 + u * kBlock + t;
+            if (j < m) {
+                keys[begin + j] = kk[u];
+                vals[begin + j] = vv[u];
+            }
+        }
+    }
+#ifdef HIDEGS_QUEUE_TRACE
+    wave_stores_done();
+    __syncthreads();
+#endif
+    WSTAMP(7);
+}
+
 union SegLds {
     SegShared lsd;
     BucketShared bucket;
@@ -1144,6 +1440,12 @@ union SegLds {
         uint32_t list[kBlock];  // segment_sort_kernel's scouts: the hot tiles of one sweep
         uint32_t nlist;
     } queue;
+};
+
+// big_segment_kernel's LDS: the queue forms, or one WIDE job's buffers (152 KB: one worker per CU)
+union QueueLds {
+    SegLds seg;
+    WideShared wide;
 };
 
 // One segment of m <= kSegCap pairs sorted by the low 32 key bits: the bucket form, or its LSD
@@ -1439,7 +1741,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
             const uint32_t nl = lds.queue.nlist;  // workgroup-uniform
             for (uint32_t j = 0; j < nl; j++) {
                 const uint32_t sg2 = list[j], b = starts[sg2], mm = starts[sg2 + 1] - b;
-                if (mm <= (uint32_t)kOpenLocal) {
+                if (HIDEGS_WIDE_SCOUTS && mm <= (uint32_t)kWideCap) {  // one WIDE job (a queue worker sorts it in LDS)
+                    if (threadIdx.x == 0) {
+                        runs_begin(lds.queue.emit);
+                        add_run(lds.queue.emit, J_WIDE, 0u, b, mm, 1u);
+                    }
+                    emit_jobs(q, lds.queue.emit);
+                } else if (mm <= (uint32_t)kOpenLocal) {
                     open_local(keys, vals, q, b, mm, lds.queue.big, lds.queue.emit, s_and, s_or);
                 } else {
                     if (threadIdx.x == 0) {
@@ -1633,10 +1941,11 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                                                              uint64_t* __restrict__ alt_k,
                                                              uint32_t* __restrict__ alt_v, const BigQueue q)
 {
-    __shared__ __attribute__((aligned(16))) SegLds lds;
+    __shared__ __attribute__((aligned(16))) QueueLds qlds;
     __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock], s_max[kWavesPerBlock];
     __shared__ uint4 s_job;
     __shared__ uint32_t s_flag;
+    SegLds& lds = qlds.seg;
     const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
     BigShared& sh = lds.queue.big;
     EmitShared& e = lds.queue.emit;
@@ -1683,7 +1992,9 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
         const uint32_t type = job.x & 0xffu, src = job.x >> 8;
         if (type == J_EXIT) return;
 
-        if (type == J_SMALL) {
+        if (type == J_WIDE) {
+            wide_sort(keys, vals, alt_k, alt_v, job.y, job.z, src, qlds.wide);
+        } else if (type == J_SMALL) {
             if (src)
                 sort_segment<false>(alt_k, alt_v, keys, vals, job.y, job.z, lds, s_and, s_or, s_max);
             else
@@ -2168,6 +2479,19 @@ uint32_t hidegs_higher_msb(uint32_t n)
 
 #ifdef HIDEGS_QUEUE_TRACE
 // experiments only: copy out (and reset) the partition queue's job trace; returns the job count
+int hidegs_debug_wide_trace(unsigned long long* host, int max_jobs)
+{
+    unsigned int n = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(&n, HIP_SYMBOL(hidegs::g_wtrace_n), sizeof(n)) != hipSuccess)
+        return -1;
+    const int m = (int)(n < (unsigned)max_jobs ? n : (unsigned)max_jobs);
+    if (m > 0 && hipMemcpyFromSymbol(host, HIP_SYMBOL(hidegs::g_wtrace), (size_t)m * 9 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    n = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hidegs::g_wtrace_n), &n, sizeof(n)) != hipSuccess) return -1;
+    return m;
+}
+
 int hidegs_debug_queue_trace(unsigned long long* host, int max_jobs)
 {
     unsigned int n = 0;

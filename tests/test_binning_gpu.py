@@ -403,6 +403,35 @@ def test_many_hot_tiles_spread_over_the_scouts(T, count, lo, hi):
     assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
 
 
+def test_wide_jobs_at_their_bounds():
+    """Tiles of 2049..12288 pairs are one WIDE job (a queue worker's LDS sort): the bounds 2049 / 12288 /
+    12289, a tile of equal depths, a tile of 3 distinct depths (long ties: stability), and a 300K tile
+    whose level-1 digits become WIDE jobs reading the alternate buffer -- bit-identical, ranges exact."""
+    T = 4096
+    g = np.random.default_rng(33)
+    keys, _ = raster_like_keys(400_000, T, 33)
+    sizes = [2049, 2050, 5000, 12287, 12288, 12289, 20000, 300_000]
+    tiles = g.choice(T, len(sizes) + 2, replace=False).astype(np.uint64)
+    parts = [keys]
+    for tile, n in zip(tiles, sizes):
+        parts.append((tile << np.uint64(32)) | g.uniform(0.5, 60.0, n).astype(np.float32).view(np.uint32).astype(np.uint64))
+    parts.append((tiles[-2] << np.uint64(32)) | np.full(7000, np.float32(3.5).view(np.uint32), np.uint64))
+    three = np.array([1.5, 2.5, 9.0], np.float32).view(np.uint32).astype(np.uint64)
+    parts.append((tiles[-1] << np.uint64(32)) | three[g.integers(0, 3, 9000)])
+    keys = np.concatenate(parts)
+    keys = keys[g.permutation(keys.size)]
+    vals = np.arange(keys.size, dtype=np.uint32)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
+    kd, vd = u64(keys), u32(vals)
+    for _ in range(2):
+        ko, vo, r = primitives.sort_tile_pairs(kd, vd, T)
+        assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+        assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+        assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
+    ko, vo = primitives.sort_pairs(kd, vd, 0, 32 + primitives.higher_msb(T))
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+
+
 def test_one_workgroup_global_form_variant():
     """The one-workgroup global form (four LSD passes through the alternate buffer) sorts tiles of
     2049..8192 pairs in a build with HIDEGS_QUEUE_MIN=8192 (build.VARIANTS['gform']); the product build

@@ -14,11 +14,16 @@ import torch  # noqa: E402
 
 from hidegs_amd import _lib, primitives, synthetic  # noqa: E402
 
-NAMES = {1: "SMALL", 2: "COPY", 3: "REDUCE", 4: "HIST", 5: "SCATTER", 6: "GLOBAL"}
+NAMES = {1: "SMALL", 2: "COPY", 3: "REDUCE", 4: "HIST", 5: "SCATTER", 6: "GLOBAL", 7: "WIDE"}
 L = _lib.lib()
 fn = L.hidegs_debug_queue_trace
 fn.restype = C.c_int
 fn.argtypes = [C.c_void_p, C.c_int]
+wfn = L.hidegs_debug_wide_trace
+wfn.restype = C.c_int
+wfn.argtypes = [C.c_void_p, C.c_int]
+wbuf = np.zeros((4096, 9), np.uint64)
+WPHASES = ["load+copy", "and/or", "bucket hist", "scan", "fill", "rank", "(lsd)", "gather"]
 
 CAP = 32768
 buf = np.zeros((CAP, 4), np.uint64)
@@ -38,8 +43,17 @@ for spec in sys.argv[1:] or ["4096", "100000", "skew:0.15:0.1", "skew:0.5:0.02"]
     primitives.sort_tile_pairs(keys, wl.values, wl.num_tiles)
     torch.cuda.synchronize()
     fn(buf.ctypes.data, CAP)  # drop the warm-up's trace
+    wfn(wbuf.ctypes.data, 4096)
     primitives.sort_tile_pairs(keys, wl.values, wl.num_tiles)
     n = fn(buf.ctypes.data, CAP)
+    nw = wfn(wbuf.ctypes.data, 4096)
+    if nw > 0:
+        wt = wbuf[:nw].astype(np.int64)
+        ok = (wt[:, 1:] > 0).all(axis=1)  # jobs that took every stamp (the bucket form and the gather)
+        d = np.diff(wt[ok, 1:], axis=1) / 100.0
+        print(f"  WIDE phases over {int(ok.sum())} of {nw} jobs (m p50 {int(np.median(wt[:, 0]))}), p50 us: " +
+              ", ".join(f"{nm} {np.median(d[:, k]):.1f}" for k, nm in enumerate(WPHASES[1:])) +
+              f"; load+copy {np.median(np.diff(wt[ok, 1:3], axis=1)) / 100.0:.1f}" if ok.any() else "")
     tr = buf[:n].copy()
     t0 = tr[:, 1].min()
     rel = (tr[:, 1:].astype(np.int64) - int(t0)) / 100.0
