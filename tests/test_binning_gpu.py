@@ -403,10 +403,7 @@ def test_many_hot_tiles_spread_over_the_scouts(T, count, lo, hi):
     assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
 
 
-def test_wide_jobs_at_their_bounds():
-    """Tiles of 2049..12288 pairs are one WIDE job (a queue worker's LDS sort): the bounds 2049 / 12288 /
-    12289, a tile of equal depths, a tile of 3 distinct depths (long ties: stability), and a 300K tile
-    whose level-1 digits become WIDE jobs reading the alternate buffer -- bit-identical, ranges exact."""
+def _wide_case():
     T = 4096
     g = np.random.default_rng(33)
     keys, _ = raster_like_keys(400_000, T, 33)
@@ -422,6 +419,14 @@ def test_wide_jobs_at_their_bounds():
     keys = keys[g.permutation(keys.size)]
     vals = np.arange(keys.size, dtype=np.uint32)
     ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
+    return T, keys, vals, ek, ev
+
+
+def test_wide_jobs_at_their_bounds():
+    """A 300K-pair tile's level-1 digits of 2049..12288 pairs are WIDE jobs (a queue worker's LDS sort
+    from the alternate buffer); with them, tiles at the bounds 2049 / 12288 / 12289, a tile of equal
+    depths and one of 3 distinct depths (long ties: stability) -- bit-identical, ranges exact."""
+    T, keys, vals, ek, ev = _wide_case()
     kd, vd = u64(keys), u32(vals)
     for _ in range(2):
         ko, vo, r = primitives.sort_tile_pairs(kd, vd, T)
@@ -430,6 +435,19 @@ def test_wide_jobs_at_their_bounds():
         assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
     ko, vo = primitives.sort_pairs(kd, vd, 0, 32 + primitives.higher_msb(T))
     assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+
+
+def test_wide_jobs_in_place_variant():
+    """The scouts' WIDE form (build.VARIANTS['wscout'], off in the product build): hot tiles of
+    2049..12288 pairs sorted in place by one WIDE job each (copied to the alternate buffer first)."""
+    from hidegs_amd import _lib, build
+    var = _lib.load_library(build.variant_path("wscout"))
+    T, keys, vals, ek, ev = _wide_case()
+    rc, ko, vo, r = _variant_sort_tile_pairs(var, u64(keys), u32(vals), T)
+    assert rc == 0
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
 
 
 def test_one_workgroup_global_form_variant():
