@@ -44,9 +44,11 @@ def main():
             torch.cuda.synchronize()
             seg_ms, seg_n = kt.get("segment_sort")
             q_ms, q_n = kt.get("big_segments")
+            sc_ms, sc_n = kt.get("radix_scatter_u64")
         print(f"{spec:>9}: K {wl.num_pairs:8d}  max tile {int(counts.max()):6d}  tiles >8192 {int((counts > 8192).sum()):3d}"
               f" >2048 {int((counts > 2048).sum()):3d}  sort {statistics.median(times):7.1f} us"
-              f"  segment_sort {seg_ms * 1e3 / max(seg_n, 1):7.1f}  big_segments {q_ms * 1e3 / max(q_n, 1):7.1f}"
+              f"  scatter {sc_ms * 1e3 / max(sc_n, 1):6.1f}  segment_sort {seg_ms * 1e3 / max(seg_n, 1):7.1f}"
+              f"  big_segments {q_ms * 1e3 / max(q_n, 1):7.1f}"
               f"  {'bit-exact' if ok else 'MISMATCH'}  qerr {qerr}", flush=True)
         del sc, wl, counts, ko, vo, perm
 
