@@ -527,3 +527,22 @@ def test_debug_mode_passes_clean_sorts():
         primitives.set_debug(False)
     ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
     assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+
+
+@pytest.mark.parametrize("cluster", [None, (0.05, 0.1), (0.15, 0.1), (0.5, 0.02)])
+def test_d2_views_sort_tile_pairs(cluster):
+    """The bench's own workloads (synthetic.d2_binning_workload): a 2M-Gaussian 1080p D2 view, and views
+    with a fraction of the Gaussians in one disc (many 2K-21K-pair tiles; one 819K-pair tile) -- the
+    whole binning sort and tile ranges bit-identical to the oracle's stable sort."""
+    from hidegs_amd import synthetic
+    cam = synthetic.d2_camera(1920, 1080)
+    wl = synthetic.d2_binning_workload(synthetic.d2_scene(2_000_000, cam, seed=1000, cluster=cluster), cam)
+    keys = wl.keys.numpy().view(np.uint64)
+    vals = wl.values.numpy().view(np.uint32)
+    T = wl.num_tiles
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
+    ko, vo, r = primitives.sort_tile_pairs(wl.keys.cuda(), wl.values.cuda(), T)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
+
