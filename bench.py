@@ -32,6 +32,8 @@ on this path is measured for real, at the configuration the metric is quoted on 
               collective at N = 1), HIP-event timed; algbw and ring busbw.  exchange_bf16: the same
               with the bf16 wire (all-to-all + fp32 sums + all-gather; view_dp.py, transport="bf16").
   exchange_and_step = the exchange followed by the masked step, sequential and overlapped.
+  dp_step   = the rank's binning step + exchange_and_step, per wire format: the built part of one
+              view-DP training step (views/s over all ranks; no rasterizer), for the scaling runs.
   masked Adam = the fused row-masked optimizer step at 2M Gaussians (59 fp32 each), 90% visible.
   cpu_baseline = on rank 0 at N = 1, every CPU leg on the same `cores` threads (the box's CPU
               share, OMP_NUM_THREADS): the oracle's OpenMP stable radix sort of the same pairs
@@ -403,6 +405,7 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
                                "speedup_vs_reference_ops": round(ref_ms / ad_ms, 2)}
         ctx["adam_state"] = (prm, opt, vis, g)
     ctx["binning_pairs"] = (wl, end_bit, sort_us)
+    ctx["binning_step"] = step
 
 
 def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, GradArena, ViewDPExchange):
@@ -449,6 +452,18 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
         line["exchange_and_step"] = {"world": world, "sequential_ms": round(seq_ms, 3),
                                      "overlapped_ms": round(fused_ms, 3), "overlapped_bf16_ms": round(bf16_ms, 3),
                                      "collectives": ex2.last.collectives, "union_rows": ex2.last.union_rows}
+        bin_step = ctx.get("binning_step")
+        if bin_step is not None:
+            # what this build runs of one view-DP training step, the rasterizer aside: the rank's view's
+            # binning, the exchange and the masked optimizer step (overlapped), per wire format
+            dp = {"world": world, "includes": "binning step + view-DP exchange + masked Adam (overlapped); "
+                                              "no rasterizer fwd/bwd (refused)"}
+            for tag, exn in (("fp32", ex2), ("bf16", ex3)):
+                ms, _ = timed(lambda: (bin_step(), exn.exchange_and_step(arena2, vis, opt, prm, max_stats=[norm2])),
+                              10, 2)
+                dp[f"{tag}_ms_per_step"] = round(ms, 3)
+                dp[f"{tag}_views_per_s_all_ranks"] = round(world / (ms * 1e-3), 1)
+            line["dp_step"] = dp
 
 
 def _cpu_baselines(line, ctx, N, cam, np):

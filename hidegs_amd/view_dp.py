@@ -133,7 +133,7 @@ class GradArena:
 
 @dataclass
 class ExchangeStats:
-    union_rows: int = 0
+    union_rows: int = 0     # rows visible to some rank (-1: not counted, a one-rank group)
     reduced_bytes: int = 0  # fp32 gradient bytes summed over ranks (per rank)
     wire_bytes: int = 0     # bytes this rank handed to the collectives for them (bf16: half)
     collectives: int = 0
@@ -285,22 +285,23 @@ class ViewDPExchange:
             if union.dtype != torch.bool or union.dim() != 1 or union.numel() != n:
                 raise ValueError(f"union must be a bool mask of the {n} gradient rows "
                                  "(fullP rows: scatter hierarchy render_indices/parent_indices into it)")
+        if self.debug and union is not None and n:
+            outside = ~union
+            for g in tensors:
+                if bool(g.reshape(n, -1)[outside].ne(0).any()):
+                    raise RuntimeError("view-DP: a gradient row outside the visibility union is non-zero; "
+                                       "the compacted exchange would desynchronise the replicas")
+        if dist.get_world_size(self.group) == 1:  # one rank: the sum is the input, in place already
+            self.last.union_rows = -1  # not counted: no host synchronisation on the one-rank path
+            return
         rows = None
         if union is not None and n:
             nu = int(union.sum())
             self.last.union_rows = nu
             if nu < self.compact_below * n:
                 rows = union.nonzero().flatten()
-            if self.debug:
-                outside = ~union
-                for g in tensors:
-                    if bool(g.reshape(n, -1)[outside].ne(0).any()):
-                        raise RuntimeError("view-DP: a gradient row outside the visibility union is non-zero; "
-                                           "the compacted exchange would desynchronise the replicas")
         else:
             self.last.union_rows = n
-        if dist.get_world_size(self.group) == 1:  # one rank: the sum is the input, in place already
-            return
         if rows is None:
             self.last.compacted = False
             if arena is not None:
@@ -394,7 +395,7 @@ class ViewDPExchange:
         union, count = self.gather_visibility(visible)
         n = arena.n
         world = dist.get_world_size(self.group)
-        nu = int(union.sum()) if n else 0
+        nu = int(union.sum()) if n and world > 1 else 0  # (no host synchronisation on one rank)
         if world == 1 or n == 0 or nu < self.compact_below * n:
             self.sum_gradients(arena, union)
             optimizer.begin_step(union).run()  # counters advance only once the gradients are summed
