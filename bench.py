@@ -28,6 +28,7 @@ on this path is measured for real, at the configuration the metric is quoted on 
   distCUDA2 = simple_knn._C.distCUDA2 on the 2M D2 centres, with its issue-rate roofline (VALU
               wave-instructions per second from the committed PMC summary, against the chip's).
   config5_scale = the binning step and distCUDA2 at config 5's size (10M Gaussians, 4K frame).
+              binning_skewed and config5_scale are single-GPU sub-metrics: measured at N = 1 only.
   exchange  = the view-DP exchange of 2M x 59 fp32 leaf gradients + stats over RCCL (no
               collective at N = 1), HIP-event timed; algbw and ring busbw.  exchange_bf16: the same
               with the bf16 wire (all-to-all + fp32 sums + all-gather; view_dp.py, transport="bf16").
@@ -307,7 +308,7 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
     line["ms_per_step_binning"] = round(ms_step, 4)
 
     # ---- the same step on a skewed view (hot tiles through the partition queue) ----------------
-    if not args.no_skewed:
+    if not args.no_skewed and world == 1:  # single-GPU sub-metric (N > 1 ranks skip its CPU-side scene)
         sk_scene = synthetic.d2_scene(N, cam, seed=1000 + rank, cluster=SKEW_CLUSTER)
         wls = synthetic.d2_binning_workload(sk_scene, cam, device=dev)
         counts = torch.bincount((wls.keys >> 32).long(), minlength=wls.num_tiles)
@@ -348,7 +349,7 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
     line["distCUDA2"] = kd
 
     # ---- config 5's scale: 10M Gaussians, 3840x2160 frame ----------------------------------------
-    if not args.no_config5:
+    if not args.no_config5 and world == 1:  # single-GPU sub-metric (a 10M scene per rank is CPU time)
         cam5 = synthetic.d2_camera(3840, 2160)
         sc5 = synthetic.d2_scene(10_000_000, cam5, seed=rank)
         wl5 = synthetic.d2_binning_workload(sc5, cam5, device=dev)
