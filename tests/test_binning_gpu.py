@@ -546,3 +546,23 @@ def test_d2_views_sort_tile_pairs(cluster):
     assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
     assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
 
+
+@pytest.mark.parametrize("case", ["one_tile_uniform", "one_tile_equal", "two_tiles_halves"])
+def test_whole_input_in_one_or_two_tiles(case):
+    """The partition queue at its extreme: every one of 4M pairs in one tile (uniform depths: records
+    four levels deep with WIDE pieces; equal keys: no varying bit at all), or split between two tiles --
+    bit-identical to the oracle, the queue's error word clear."""
+    g = np.random.default_rng(sum(map(ord, case)))
+    n, T = 4_000_000, 8160
+    if case == "one_tile_equal":
+        keys = np.full(n, (np.uint64(4321) << np.uint64(32)) | np.uint64(0x40490fdb), np.uint64)
+    else:
+        tiles = np.full(n, 77, np.uint64) if case == "one_tile_uniform" else g.choice(np.array([5, 8000], np.uint64), n)
+        keys = (tiles << np.uint64(32)) | g.uniform(0.2, 100.0, n).astype(np.float32).view(np.uint32).astype(np.uint64)
+    vals = np.arange(n, dtype=np.uint32)
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
+    ko, vo, r = primitives.sort_tile_pairs(u64(keys), u32(vals), T)
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
+
