@@ -571,6 +571,15 @@ __device__ __forceinline__ void wave_and_or(uint32_t& a, uint32_t& o)
     }
 }
 
+__device__ __forceinline__ void wave_min_max(uint32_t& lo, uint32_t& hi)
+{
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor(lo, sh, kWave));
+        hi = max(hi, (uint32_t)__shfl_xor(hi, sh, kWave));
+    }
+}
+
 // LDS of the oversized-segment forms (the one-workgroup global form, the partition jobs).
 struct BigShared {
     uint32_t cnt[kWavesPerBlock][kRadix];
@@ -788,6 +797,55 @@ constexpr int kIndexBits = 11;   // index in segment < kSegCap
 #endif
 
 static_assert(kSegCap <= (1 << kIndexBits), "segment index must fit its field");
+
+// The segment's low-key statistics for the bucket form: diff (the bits that vary: AND ^ OR) and the
+// smallest low key lo, with the bucket digit over the keys' RANGE [lo, hi]: bucket = (x - lo) >> shift
+// with shift = bits(hi - lo) - kBucketBits.  Float depth bits spread over many exponents (0.2 .. 100:
+// bits 23..30 all vary, the top ten varying bits leave ~40 of 1024 buckets in use) fill the buckets
+// evenly this way; the order is the same, x - lo being monotone over the segment.  Every thread
+// passes its own partial a / o / lo / hi; s0, s1 hold kWavesPerBlock words each.
+struct SegStats {
+    uint32_t diff, lo;
+    int shift, dbits;
+};
+__device__ __forceinline__ SegStats segment_stats(uint32_t a, uint32_t o, uint32_t lo, uint32_t hi, uint32_t* s0,
+                                                  uint32_t* s1)
+{
+    const int lane = lane_id(), wave = threadIdx.x / kWave;
+    wave_and_or(a, o);
+    wave_min_max(lo, hi);
+    if (lane == 0) {
+        s0[wave] = a;
+        s1[wave] = o;
+    }
+    __syncthreads();
+    uint32_t aa = 0xffffffffu, oo = 0u;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; w++) {
+        aa &= s0[w];
+        oo |= s1[w];
+    }
+    __syncthreads();
+    if (lane == 0) {
+        s0[wave] = lo;
+        s1[wave] = hi;
+    }
+    __syncthreads();
+    uint32_t ll = 0xffffffffu, hh = 0u;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; w++) {
+        ll = min(ll, s0[w]);
+        hh = max(hh, s1[w]);
+    }
+    SegStats st;
+    st.diff = aa ^ oo;
+    st.lo = ll;
+    const int nbits = hh > ll ? 32 - __builtin_clz(hh - ll) : 0;
+    st.dbits = nbits < kBucketBits ? nbits : kBucketBits;
+    st.shift = nbits - st.dbits;
+    return st;
+}
+
 
 struct BucketShared {
     uint32_t comb[kSegCap];   // (key bits below the digit << kIndexBits) | index, grouped by bucket
@@ -1199,7 +1257,7 @@ __device__ __forceinline__ void wide_sort(uint64_t* __restrict__ keys, uint32_t*
     const unsigned int wslot = s_wslot;
 #endif
     WSTAMP(0);
-    uint32_t a = 0xffffffffu, o = 0u;
+    uint32_t a = 0xffffffffu, o = 0u, mn = 0xffffffffu, mx = 0u;
     for (uint32_t i0 = 0; i0 < m; i0 += kBlock * kWideBatch) {  // kWideBatch loads in flight per thread
         uint64_t kk[kWideBatch];
         uint32_t vv[kWideBatch];
@@ -1220,6 +1278,8 @@ __device__ __forceinline__ void wide_sort(uint64_t* __restrict__ keys, uint32_t*
                 w.i[0][i] = (uint16_t)i;
                 a &= lo;
                 o |= lo;
+                mn = min(mn, lo);
+                mx = max(mx, lo);
                 if (!src) {
                     alt_k[begin + i] = kk[u];
                     alt_v[begin + i] = vv[u];
@@ -1227,31 +1287,17 @@ __device__ __forceinline__ void wide_sort(uint64_t* __restrict__ keys, uint32_t*
             }
         }
     }
-    wave_and_or(a, o);
-    if (lane == 0) {
-        w.red[0][wave] = a;
-        w.red[1][wave] = o;
-    }
-    __syncthreads();
-    a = 0xffffffffu;
-    o = 0u;
-#pragma unroll
-    for (int ww = 0; ww < kWavesPerBlock; ww++) {
-        a &= w.red[0][ww];
-        o |= w.red[1][ww];
-    }
-    const uint32_t diff = a ^ o;  // block-uniform
+    const SegStats st = segment_stats(a, o, mn, mx, w.red[0], w.red[1]);
+    const uint32_t diff = st.diff;  // block-uniform
     WSTAMP(1);
     int cur = 0;
-    // Bucket form (as segment_sort's): the top kBucketBits varying bits pick a bucket, and an item's
-    // place in its bucket is its exact rank by (key bits below the bucket digit || index), so equal
-    // keys keep their input order.  Its start / fill counters borrow the storage of i[0].
-    const int top = diff ? 31 - __builtin_clz(diff) : 0;
-    const int dbits = top + 1 < kBucketBits ? top + 1 : kBucketBits;
-    const int bshift = top + 1 - dbits;
+    // Bucket form (as segment_sort's): (x - lo) >> shift over the segment's key range picks a bucket,
+    // and an item's place in its bucket is its exact rank by (the bits below || index), so equal keys
+    // keep their input order.  Its start / fill counters borrow the storage of i[0].
+    const int bshift = st.shift;
+    const uint32_t base_lo = st.lo;
     bool lsd = diff != 0u;
     if (diff && bshift + kWideIndexBits <= 32) {  // block-uniform
-        const uint32_t dmask = (1u << dbits) - 1u;
         const uint32_t lowmask = (uint32_t)((1ull << bshift) - 1ull);
         uint32_t* start = reinterpret_cast<uint32_t*>(&w.i[0][0]);
         uint32_t* fill = start + kBuckets;
@@ -1266,7 +1312,7 @@ __device__ __forceinline__ void wide_sort(uint64_t* __restrict__ keys, uint32_t*
             }
 #pragma unroll
             for (int u = 0; u < kWideIlp; u++)
-                if (i0 + u * kBlock + t < m) atomicAdd(&fill[(x[u] >> bshift) & dmask], 1u);
+                if (i0 + u * kBlock + t < m) atomicAdd(&fill[(x[u] - base_lo) >> bshift], 1u);
         }
         __syncthreads();
         WSTAMP(2);
@@ -1307,11 +1353,11 @@ __device__ __forceinline__ void wide_sort(uint64_t* __restrict__ keys, uint32_t*
                 }
 #pragma unroll
                 for (int u = 0; u < kWideIlp; u++)
-                    if (i0 + u * kBlock + t < m) slot[u] = atomicAdd(&fill[(x[u] >> bshift) & dmask], 1u);
+                    if (i0 + u * kBlock + t < m) slot[u] = atomicAdd(&fill[(x[u] - base_lo) >> bshift], 1u);
 #pragma unroll
                 for (int u = 0; u < kWideIlp; u++) {
                     const uint32_t i = i0 + u * kBlock + t;
-                    if (i < m) comb[slot[u]] = ((x[u] & lowmask) << kWideIndexBits) | i;
+                    if (i < m) comb[slot[u]] = (((x[u] - base_lo) & lowmask) << kWideIndexBits) | i;
                 }
             }
             __syncthreads();
@@ -1322,8 +1368,8 @@ __device__ __forceinline__ void wide_sort(uint64_t* __restrict__ keys, uint32_t*
 #pragma unroll
                 for (int u = 0; u < kWideIlp; u++) {
                     const uint32_t i = i0 + u * kBlock + t;
-                    const uint32_t x = i < m ? w.k[0][i] : 0u;
-                    const uint32_t bk = (x >> bshift) & dmask;
+                    const uint32_t x = (i < m ? w.k[0][i] : base_lo) - base_lo;
+                    const uint32_t bk = x >> bshift;
                     me[u] = ((x & lowmask) << kWideIndexBits) | i;
                     s0[u] = start[bk];
                     e0[u] = i < m ? fill[bk] : s0[u];
@@ -1462,35 +1508,24 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
     const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
     uint64_t k[kSegItems];
     uint32_t v[kSegItems];
-    uint32_t a = 0xffffffffu, o = 0;
+    uint32_t a = 0xffffffffu, o = 0, lo = 0xffffffffu, hi = 0;
 #pragma unroll
     for (int q = 0; q < kSegItems; q++) {
         const uint32_t i = t + q * kBlock;
         if (i < m) {
             k[q] = src_k[begin + i];
             v[q] = src_v[begin + i];
-            a &= (uint32_t)k[q];
-            o |= (uint32_t)k[q];
+            const uint32_t x = (uint32_t)k[q];
+            a &= x;
+            o |= x;
+            lo = min(lo, x);
+            hi = max(hi, x);
         }
     }
     BucketShared& sh = lds.bucket;
     for (int i = t; i < kBuckets; i += kBlock) sh.fill[i] = 0u;
-    wave_and_or(a, o);
-    if (lane == 0) {
-        s_and[wave] = a;
-        s_or[wave] = o;
-    }
-    __syncthreads();
-    uint32_t diff;
-    {
-        uint32_t aa = 0xffffffffu, oo = 0;
-#pragma unroll
-        for (int w = 0; w < kWavesPerBlock; w++) {
-            aa &= s_and[w];
-            oo |= s_or[w];
-        }
-        diff = aa ^ oo;  // low key bits that vary over the segment
-    }
+    const SegStats st = segment_stats(a, o, lo, hi, s_and, s_or);
+    const uint32_t diff = st.diff;  // low key bits that vary over the segment
     if (diff == 0) {  // equal low keys: the input order is the stable order
         if (!InPlace) {
 #pragma unroll
@@ -1504,16 +1539,14 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
         }
         return;
     }
-    const int top = 31 - __builtin_clz(diff);
-    const int dbits = top + 1 < kBucketBits ? top + 1 : kBucketBits;
-    const int shift = top + 1 - dbits;
-    const uint32_t dmask = (1u << dbits) - 1u;
+    const int shift = st.shift;
+    const uint32_t base_lo = st.lo;
     const uint32_t lowmask = (uint32_t)((1ull << shift) - 1ull);
 
-    // 1. bucket histogram
+    // 1. bucket histogram (bucket = (x - lo) >> shift < 2^dbits)
 #pragma unroll
     for (int q = 0; q < kSegItems; q++)
-        if (t + q * kBlock < m) atomicAdd(&sh.fill[((uint32_t)k[q] >> shift) & dmask], 1u);
+        if (t + q * kBlock < m) atomicAdd(&sh.fill[((uint32_t)k[q] - base_lo) >> shift], 1u);
     __syncthreads();
     // 2. bucket starts (exclusive scan, 4 buckets per thread) and the fullest bucket
     uint32_t c[kBuckets / kBlock], sum = 0, mx = 0;
@@ -1554,8 +1587,9 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
     for (int q = 0; q < kSegItems; q++) {
         const uint32_t i = t + q * kBlock;
         if (i < m) {
-            bucket[q] = ((uint32_t)k[q] >> shift) & dmask;
-            me[q] = (((uint32_t)k[q] & lowmask) << kIndexBits) | i;
+            const uint32_t x = (uint32_t)k[q] - base_lo;
+            bucket[q] = x >> shift;
+            me[q] = ((x & lowmask) << kIndexBits) | i;
             sh.comb[atomicAdd(&sh.fill[bucket[q]], 1u)] = me[q];
         }
     }
@@ -1790,46 +1824,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
     const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
     uint64_t k[kSegItems];
     uint32_t v[kSegItems];
-    uint32_t a = 0xffffffffu, o = 0;
+    uint32_t a = 0xffffffffu, o = 0, lo = 0xffffffffu, hi = 0;
 #pragma unroll
     for (int q = 0; q < kSegItems; q++) {
         const uint32_t i = t + q * kBlock;
         if (i < m) {
             k[q] = keys[begin + i];
             v[q] = vals[begin + i];
-            a &= (uint32_t)k[q];
-            o |= (uint32_t)k[q];
+            const uint32_t x = (uint32_t)k[q];
+            a &= x;
+            o |= x;
+            lo = min(lo, x);
+            hi = max(hi, x);
         }
     }
     BucketShared& sh = lds.bucket;
     for (int i = t; i < kBuckets; i += kBlock) sh.fill[i] = 0u;
-    wave_and_or(a, o);
-    if (lane == 0) {
-        s_and[wave] = a;
-        s_or[wave] = o;
-    }
-    __syncthreads();
-    uint32_t diff;
-    {
-        uint32_t aa = 0xffffffffu, oo = 0;
-#pragma unroll
-        for (int w = 0; w < kWavesPerBlock; w++) {
-            aa &= s_and[w];
-            oo |= s_or[w];
-        }
-        diff = aa ^ oo;  // low key bits that vary over the segment
-    }
+    const SegStats st = segment_stats(a, o, lo, hi, s_and, s_or);
+    const uint32_t diff = st.diff;  // low key bits that vary over the segment
     if (diff == 0) return;  // equal low keys: the input order is the stable order
-    const int top = 31 - __builtin_clz(diff);
-    const int dbits = top + 1 < kBucketBits ? top + 1 : kBucketBits;
-    const int shift = top + 1 - dbits;
-    const uint32_t dmask = (1u << dbits) - 1u;
+    const int shift = st.shift;
+    const uint32_t base_lo = st.lo;
     const uint32_t lowmask = (uint32_t)((1ull << shift) - 1ull);
 
-    // 1. bucket histogram
+    // 1. bucket histogram (bucket = (x - lo) >> shift, over the segment's key range)
 #pragma unroll
     for (int q = 0; q < kSegItems; q++)
-        if (t + q * kBlock < m) atomicAdd(&sh.fill[((uint32_t)k[q] >> shift) & dmask], 1u);
+        if (t + q * kBlock < m) atomicAdd(&sh.fill[((uint32_t)k[q] - base_lo) >> shift], 1u);
     __syncthreads();
     // 2. bucket starts (exclusive scan, 4 buckets per thread) and the fullest bucket
     uint32_t c[kBuckets / kBlock], sum = 0, mx = 0;
@@ -1870,8 +1891,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
     for (int q = 0; q < kSegItems; q++) {
         const uint32_t i = t + q * kBlock;
         if (i < m) {
-            bucket[q] = ((uint32_t)k[q] >> shift) & dmask;
-            me[q] = (((uint32_t)k[q] & lowmask) << kIndexBits) | i;
+            const uint32_t x = (uint32_t)k[q] - base_lo;
+            bucket[q] = x >> shift;
+            me[q] = ((x & lowmask) << kIndexBits) | i;
             sh.comb[atomicAdd(&sh.fill[bucket[q]], 1u)] = me[q];
         }
     }

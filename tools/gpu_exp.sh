@@ -1,4 +1,2 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
-: > gpurun_out/exp.log
-for v in "" rpipe; do echo "== ${v:-default}" >> gpurun_out/exp.log; HIDEGS_LIB=${v:+variants/libhidegs_$v.so} timeout -k 10 200 python -u tools/skew_time.py none 0.15:0.1 >> gpurun_out/exp.log 2>&1 || exit 1; done
-HIDEGS_LIB=variants/libhidegs_rpipe.so timeout -k 10 300 python -u -m pytest tests/test_binning_gpu.py -m gpu -q --timeout 120 --timeout-method thread >> gpurun_out/exp.log 2>&1; echo "tests rc=$?" >> gpurun_out/exp.log
+bash tools/gpu_skew_ab.sh && timeout -k 10 300 python -u tools/extreme_time.py > gpurun_out/ext.log 2>&1
