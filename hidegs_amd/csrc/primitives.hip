@@ -152,13 +152,14 @@ __device__ __forceinline__ uint32_t digit_of(K key, int shift, uint32_t mask)
 // are equal in every item (a caller's guarantee) and need none.  The lowest lane of each
 // digit group bumps the counter (LDS ops of one wave retire in order, so the read precedes
 // the write).
-template <typename K, int R>
+// With Based, the digit is taken of (low key half - dbase) instead (the partition queue's digits).
+template <typename K, int R, bool Based = false>
 __device__ __forceinline__ void wave_rank(const K (&k)[R], const bool (&ok)[R], int shift, uint32_t mask,
-                                          uint32_t* cnt, uint32_t (&rank)[R], uint32_t vary)
+                                          uint32_t* cnt, uint32_t (&rank)[R], uint32_t vary, uint32_t dbase = 0u)
 {
 #pragma unroll
     for (int r = 0; r < R; r++) {
-        const uint32_t d = digit_of(k[r], shift, mask);
+        const uint32_t d = Based ? ((((uint32_t)k[r]) - dbase) >> shift) & mask : digit_of(k[r], shift, mask);
         const uint64_t okb = __ballot(ok[r]);
         uint32_t mlo = (uint32_t)okb, mhi = (uint32_t)(okb >> 32);  // lanes with the same digit
 #pragma unroll
@@ -585,24 +586,24 @@ struct BigShared {
     uint32_t cnt[kWavesPerBlock][kRadix];
     uint32_t hist[kRadix];
     uint32_t run[kRadix];  // running destination of each digit
-    uint32_t aux[2][kRadix];  // partition jobs: AND / OR of each digit's low key halves
+    uint32_t aux[2][kRadix];  // partition jobs: MIN / MAX of each digit's low key halves
     uint32_t wave[kWavesPerBlock];
 };
 
 // One stable step of a digit pass through global memory: the cnt <= kBigItems * kBlock items
-// [base, base + cnt) of (sk, sv) are ranked by digit (key >> shift) & mask inside the step (wave w
+// [base, base + cnt) of (sk, sv) are ranked by digit ((low key half - dbase) >> shift) & mask inside the step (wave w
 // owns items [w * 512, w * 512 + 512) in (round, lane) order) and item i goes to
 // sh.run[digit] + its rank, then sh.run advances by the step's digit counts.  sh.run must be set
 // before the call (its first barrier publishes it).  Destinations outside [lo, hi) are dropped:
 // never, for consistent offsets -- a guard, not a case.
 constexpr int kBigItems = 8;
 constexpr int kBigStep = kBigItems * kBlock;  // 2048
-// Track: also fold each item's low key half into sh.aux[0][digit] (AND) and sh.aux[1][digit] (OR).
+// Track: also fold each item's low key half into sh.aux[0][digit] (MIN) and sh.aux[1][digit] (MAX).
 template <bool Track = false>
 __device__ __forceinline__ void scatter_step(const uint64_t* sk, const uint32_t* sv, uint64_t* dk, uint32_t* dv,
-                                             const uint32_t base, const uint32_t cnt, const int shift,
-                                             const uint32_t mask, const uint32_t lo, const uint32_t hi,
-                                             BigShared& sh)
+                                             const uint32_t base, const uint32_t cnt, const uint32_t dbase,
+                                             const int shift, const uint32_t mask, const uint32_t lo,
+                                             const uint32_t hi, BigShared& sh)
 {
     const int t = threadIdx.x;
     const int lane = lane_id();
@@ -621,14 +622,14 @@ __device__ __forceinline__ void scatter_step(const uint64_t* sk, const uint32_t*
         k[q] = ok[q] ? sk[base + i] : 0ull;
         v[q] = ok[q] ? sv[base + i] : 0u;
     }
-    wave_rank<uint64_t, kBigItems>(k, ok, shift, mask, sh.cnt[wave], rank, mask);
+    wave_rank<uint64_t, kBigItems, true>(k, ok, shift, mask, sh.cnt[wave], rank, mask, dbase);
     __syncthreads();
     const uint32_t tot = digit_wave_prefix(sh.cnt);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kBigItems; q++) {
         if (ok[q]) {
-            const uint32_t dd = digit_of(k[q], shift, mask);
+            const uint32_t dd = (((uint32_t)k[q] - dbase) >> shift) & mask;
 #ifdef HIDEGS_EXP_INORDER_SCATTER  // experiments only: input-order stores (wrong result; store-pattern A/B)
             const uint32_t dst = base + w0 + q * kWave + lane;
             (void)rank;
@@ -639,10 +640,10 @@ __device__ __forceinline__ void scatter_step(const uint64_t* sk, const uint32_t*
                 dk[dst] = k[q];
                 dv[dst] = v[q];
             }
-#ifndef HIDEGS_EXP_NO_TRACK  // experiments only: no per-digit AND / OR (wrong next-level digits; cost A/B)
+#ifndef HIDEGS_EXP_NO_TRACK  // experiments only: no per-digit MIN / MAX (wrong next-level digits; cost A/B)
             if (Track) {
-                atomicAnd(&sh.aux[0][dd], (uint32_t)k[q]);
-                atomicOr(&sh.aux[1][dd], (uint32_t)k[q]);
+                atomicMin(&sh.aux[0][dd], (uint32_t)k[q]);
+                atomicMax(&sh.aux[1][dd], (uint32_t)k[q]);
             }
 #endif
         }
@@ -673,8 +674,8 @@ __device__ __forceinline__ void segment_sort_global(uint64_t* __restrict__ keys,
         uint32_t dummy;
         sh.run[t] = begin + block_exclusive_scan(sh.hist[t], sh.wave, &dummy);
         for (uint32_t c0 = 0; c0 < m; c0 += kBigStep)
-            scatter_step(sk, sv, dk, dv, begin + c0, m - c0 < (uint32_t)kBigStep ? m - c0 : (uint32_t)kBigStep, shift,
-                         kRadix - 1, begin, begin + m, sh);
+            scatter_step(sk, sv, dk, dv, begin + c0, m - c0 < (uint32_t)kBigStep ? m - c0 : (uint32_t)kBigStep, 0u,
+                         shift, kRadix - 1, begin, begin + m, sh);
     }
 }
 
@@ -862,7 +863,7 @@ static_assert(sizeof(BucketShared) >= kSegRun * (sizeof(uint64_t) + sizeof(uint3
 // A segment of more than kSegCap pairs is not sorted by one workgroup (that costs ~10 ns per pair:
 // a 100K-pair tile took 1 ms) but split among many.  It becomes a RECORD, partitioned stably by
 // one digit -- its top <= 8 varying low-key bits -- in three phases of chunk jobs (kChunk pairs):
-//   REDUCE   AND / OR of the chunk's low key halves        -> the digit (last chunk decides)
+//   REDUCE   MIN / MAX of the chunk's low key halves       -> the digit (last chunk decides)
 //   HIST     the chunk's digit counts                      -> pool; the last chunk scans them into
 //                                                             every chunk's per-digit destinations
 //   SCATTER  the chunk's pairs, ranked stably, to the other buffer (keys <-> alt)
@@ -912,12 +913,13 @@ static_assert(Q_WORDS <= kBlock, "identify_ranges_kernel zeroes the counters wit
 
 struct BigSeg {
     uint32_t begin, m, src, chunks;  // pairs [begin, begin + m) of keys (src 0) or alt (src 1)
-    uint32_t and_bits, or_bits;      // REDUCE: AND / OR of the low key halves
-    uint32_t shift, bits;            // the digit: key bits [shift, shift + bits)
+    uint32_t lo_bits, hi_bits;       // REDUCE: MIN / MAX of the low key halves
+    uint32_t shift, bits;            // the digit: bits [shift, shift + bits) of (low key half - lo)
+    uint32_t lo;                     // the digit's base: the record's smallest low key half
     uint32_t pool;                   // (chunks + 2) x 256 u32: per-chunk counts -> destinations,
                                      // then the digit starts and the digit totals
     uint32_t pending;                // jobs of the current phase not yet finished
-    uint32_t pad[2];
+    uint32_t pad[1];
 };
 
 struct BigQueue {
@@ -1000,26 +1002,40 @@ __device__ __forceinline__ uint4 run_job(const uint4 r, const uint32_t j)
     return make_uint4(r.x, r.y, r.z, 0u);
 }
 
-// The digit of a record whose varying low-key bits are `diff`: its top <= 8 of them.
-__device__ __forceinline__ void set_digit(BigSeg& s, uint32_t diff)
+// A record's digit over its low keys' range [lo, hi] (lo < hi): the top <= 8 bits of x - lo.  Float
+// depth bits that cross exponent boundaries vary in every exponent bit; a digit of the top varying
+// bits would then split by exponent only (a few crowded digits), one of the range splits the mass.
+__device__ __forceinline__ void range_digit(uint32_t lo, uint32_t hi, int& shift, int& bits)
 {
-    const int top = 31 - __builtin_clz(diff);
-    const int bits = top + 1 < kRadixBits ? top + 1 : kRadixBits;
-    s.shift = (uint32_t)(top + 1 - bits);
+    const int nbits = 32 - __builtin_clz(hi - lo);
+    bits = nbits < kRadixBits ? nbits : kRadixBits;
+    shift = nbits - bits;
+}
+__device__ __forceinline__ void set_digit(BigSeg& s, uint32_t lo, uint32_t hi)
+{
+    int shift, bits;
+    range_digit(lo, hi, shift, bits);
+    s.lo = lo;
+    s.shift = (uint32_t)shift;
     s.bits = (uint32_t)bits;
+}
+// digit of a pair of a record: bits [shift, shift + bits) of (low key half - lo)
+__device__ __forceinline__ uint32_t rec_digit(uint64_t key, uint32_t lo, int shift, uint32_t mask)
+{
+    return (((uint32_t)key - lo) >> shift) & mask;
 }
 
 // A new record over [begin, begin + m) of buffer src, as the run of jobs that starts it: REDUCE
-// chunk jobs, or -- when the varying bits are known already (`diff` from the parent's SCATTER;
-// ~0u: unknown) -- HIST chunk jobs right away, or a COPY / nothing for a piece with no varying
-// bit.  With the record table or the pool full: one GLOBAL job (the one-workgroup sort).
+// chunk jobs, or -- when the low keys' range [lo, hi] is known already (from the parent's SCATTER or
+// the opener; `known` false: unknown) -- HIST chunk jobs right away, or a COPY / nothing for a piece
+// of equal low keys.  With the record table or the pool full: one GLOBAL job (the one-workgroup sort).
 // The pool holds (chunks + 4) x 256 u32: per-chunk counts -> destinations, then the digit starts,
-// totals, and AND / OR of each digit's low key halves (the next level's `diff`).
+// totals, and MIN / MAX of each digit's low key halves (the next level's range).
 __device__ __forceinline__ uint4 record_run(const BigQueue& q, uint32_t begin, uint32_t m, uint32_t src,
-                                            uint32_t diff)
+                                            bool known, uint32_t lo, uint32_t hi)
 {
     const uint32_t chunks = (m + kChunk - 1) / kChunk;
-    if (diff == 0u) return make_uint4(J_COPY | (src << 8), begin, m, src ? chunks : 0u);  // already in order
+    if (known && lo == hi) return make_uint4(J_COPY | (src << 8), begin, m, src ? chunks : 0u);  // already in order
     const uint32_t need = (chunks + 4) * kRadix;
     const uint32_t r = __hip_atomic_fetch_add(&q.ctl[kCtlStride * Q_NREC], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t p = ~0u;
@@ -1033,14 +1049,15 @@ __device__ __forceinline__ uint4 record_run(const BigQueue& q, uint32_t begin, u
     s.m = m;
     s.src = src;
     s.chunks = chunks;
-    s.and_bits = 0xffffffffu;
-    s.or_bits = 0u;
+    s.lo_bits = 0xffffffffu;
+    s.hi_bits = 0u;
     s.shift = 0u;
     s.bits = 0u;
+    s.lo = 0u;
     s.pool = p;
     s.pending = chunks;
-    if (diff == ~0u) return make_uint4(J_REDUCE, r, 0u, chunks);
-    set_digit(s, diff);
+    if (!known) return make_uint4(J_REDUCE, r, 0u, chunks);
+    set_digit(s, lo, hi);
     return make_uint4(J_HIST, r, 0u, chunks);
 }
 
@@ -1086,7 +1103,7 @@ __device__ __forceinline__ void emit_jobs(const BigQueue& q, EmitShared& e)
 
 // Thread t's result: the number of the cnt <= kChunk keys at sk[base..] whose digit is t.
 __device__ __forceinline__ uint32_t chunk_hist(const uint64_t* sk, const uint32_t base, const uint32_t cnt,
-                                               const int shift, const uint32_t mask, BigShared& sh)
+                                               const uint32_t lo, const int shift, const uint32_t mask, BigShared& sh)
 {
     const int t = threadIdx.x;
     sh.hist[t] = 0u;
@@ -1095,7 +1112,7 @@ __device__ __forceinline__ uint32_t chunk_hist(const uint64_t* sk, const uint32_
 #pragma unroll
     for (int u = 0; u < kChunk / kBlock; u++) {
         const uint32_t i = t + u * kBlock;
-        dg[u] = i < cnt ? digit_of(sk[base + i], shift, mask) : ~0u;
+        dg[u] = i < cnt ? rec_digit(sk[base + i], lo, shift, mask) : ~0u;
     }
 #pragma unroll
     for (int u = 0; u < kChunk / kBlock; u++)
@@ -1106,7 +1123,7 @@ __device__ __forceinline__ uint32_t chunk_hist(const uint64_t* sk, const uint32_
 
 // After every chunk's counts are in the record's pool (col = this thread's digit column): every
 // chunk's destination of each digit (begin + digit start + the digit's count in the chunks before
-// it), the digit starts and totals, and the AND / OR rows the SCATTER jobs gather into.
+// it), the digit starts and totals, and the MIN / MAX rows the SCATTER jobs gather into.
 __device__ __forceinline__ void plan_scatter(uint32_t* col, const uint32_t chunks, const uint32_t begin, BigShared& sh)
 {
     constexpr uint32_t U = 8;  // independent loads in flight: the column is in other XCDs' writes
@@ -1138,7 +1155,7 @@ __device__ __forceinline__ void plan_scatter(uint32_t* col, const uint32_t chunk
 }
 
 // The last chunk of a record's SCATTER phase (all of its pairs are in buffer dst, and col -- this
-// thread's digit column of the record's pool -- holds the digit starts, totals and AND / OR rows):
+// thread's digit column of the record's pool -- holds the digit starts, totals and MIN / MAX rows):
 // cut the record into the pieces the queue sorts next, as runs in e (thread 0 publishes them with
 // emit_jobs).  Every thread of the workgroup calls it.
 __device__ __forceinline__ void cut_pieces(const BigQueue& q, EmitShared& e, BigShared& sh, const uint32_t* col,
@@ -1154,7 +1171,7 @@ __device__ __forceinline__ void cut_pieces(const BigQueue& q, EmitShared& e, Big
     //    a kSegRun-aligned window (so a piece holds < 2 * kSegRun = kSegCap pairs).
     const uint32_t n_d = col[(chunks + 1) * kRadix];  // 0 above the digit mask
     const uint32_t s_d = col[chunks * kRadix];        // relative start
-    const uint32_t diff_d = col[(chunks + 2) * kRadix] ^ col[(chunks + 3) * kRadix];
+    const uint32_t lo_d = col[(chunks + 2) * kRadix], hi_d = col[(chunks + 3) * kRadix];  // the digit's range
     if (shift == 0) {  // every varying bit is placed: the record is sorted
         if (t == 0) {
             runs_begin(e);
@@ -1190,7 +1207,7 @@ __device__ __forceinline__ void cut_pieces(const BigQueue& q, EmitShared& e, Big
         if (boundary) {
             if (n_d > (uint32_t)kSegCap)
                 run = n_d <= (uint32_t)kWideCap ? make_uint4(J_WIDE | (dst << 8), begin + s_d, n_d, 1u)
-                                                : record_run(q, begin + s_d, n_d, dst, diff_d);
+                                                : record_run(q, begin + s_d, n_d, dst, true, lo_d, hi_d);
             else if (next - s_d > 1u || dst)
                 run = make_uint4(J_SMALL | (dst << 8), begin + s_d, next - s_d, 1u);
         }
@@ -1649,7 +1666,7 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
 #endif
 constexpr int kOpenLocal = HIDEGS_OPEN_LOCAL;
 #ifndef HIDEGS_SCATTER_LOCAL
-#define HIDEGS_SCATTER_LOCAL 8192  // ... and up to this many, its SCATTER phase too
+#define HIDEGS_SCATTER_LOCAL 0  // ... and up to this many, its SCATTER phase too (0: never; DESIGN.md, range digits)
 #endif
 constexpr int kScatterLocal = HIDEGS_SCATTER_LOCAL;
 #ifndef HIDEGS_SCOUTS
@@ -1665,35 +1682,34 @@ __device__ __forceinline__ void open_local(const uint64_t* keys, const uint32_t*
                                            uint32_t* s_or)
 {
     const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
-    uint32_t a = 0xffffffffu, o = 0u;
+    uint32_t lo = 0xffffffffu, hi = 0u;
     for (uint32_t i0 = 0; i0 < m; i0 += kChunk) {
         uint32_t x[kChunk / kBlock];
 #pragma unroll
         for (int u = 0; u < kChunk / kBlock; u++) {
             const uint32_t i = i0 + u * kBlock + t;
-            x[u] = (uint32_t)keys[begin + (i < m ? i : 0u)];  // a repeat changes no AND / OR
+            x[u] = (uint32_t)keys[begin + (i < m ? i : 0u)];  // a repeat changes no MIN / MAX
         }
 #pragma unroll
         for (int u = 0; u < kChunk / kBlock; u++) {
-            a &= x[u];
-            o |= x[u];
+            lo = min(lo, x[u]);
+            hi = max(hi, x[u]);
         }
     }
-    wave_and_or(a, o);
+    wave_min_max(lo, hi);
     if (lane == 0) {
-        s_and[wave] = a;
-        s_or[wave] = o;
+        s_and[wave] = lo;
+        s_or[wave] = hi;
     }
     __syncthreads();
     for (int w = 0; w < kWavesPerBlock; w++) {
-        a &= s_and[w];
-        o |= s_or[w];
+        lo = min(lo, s_and[w]);
+        hi = max(hi, s_or[w]);
     }
-    const uint32_t diff = a ^ o;
-    if (diff == 0u) return;  // equal low keys: in stable order already (block-uniform)
+    if (lo == hi) return;  // equal low keys: in stable order already (block-uniform)
     if (t == 0) {
         runs_begin(e);
-        const uint4 r = record_run(q, begin, m, 0u, diff);
+        const uint4 r = record_run(q, begin, m, 0u, true, lo, hi);
         e.run[0] = r;
         e.base = (r.x & 0xffu) == J_HIST ? q.rec[r.y].pool : ~0u;
         if (e.base == ~0u) add_run(e, r);  // the table or pool is full: a GLOBAL job
@@ -1701,15 +1717,14 @@ __device__ __forceinline__ void open_local(const uint64_t* keys, const uint32_t*
     __syncthreads();
     const uint32_t pool = e.base, rec = e.run[0].y, chunks = (m + kChunk - 1) / kChunk;
     if (pool != ~0u) {
-        const int top = 31 - __builtin_clz(diff);  // the record's digit (set_digit)
-        const int bits = top + 1 < kRadixBits ? top + 1 : kRadixBits;
-        const int shift = top + 1 - bits;
+        int shift, bits;
+        range_digit(lo, hi, shift, bits);  // the record's digit (set_digit)
         const uint32_t mask = (1u << bits) - 1u;
         uint32_t* col = q.pool + pool + t;
         for (uint32_t c = 0; c < chunks; c++) {
             const uint32_t c0 = c * kChunk;
             col[c * kRadix] = chunk_hist(keys, begin + c0, m - c0 < (uint32_t)kChunk ? m - c0 : (uint32_t)kChunk,
-                                         shift, mask, sh);
+                                         lo, shift, mask, sh);
         }
         __syncthreads();
         plan_scatter(col, chunks, begin, sh);
@@ -1722,8 +1737,8 @@ __device__ __forceinline__ void open_local(const uint64_t* keys, const uint32_t*
                 sh.run[t] = col[c * kRadix];
                 for (uint32_t b = 0; b < cnt; b += kBigStep)
                     scatter_step<true>(keys, vals, q.alt_k, q.alt_v, begin + c0 + b,
-                                       cnt - b < (uint32_t)kBigStep ? cnt - b : (uint32_t)kBigStep, shift, mask, begin,
-                                       begin + m, sh);
+                                       cnt - b < (uint32_t)kBigStep ? cnt - b : (uint32_t)kBigStep, lo, shift, mask,
+                                       begin, begin + m, sh);
             }
             col[(chunks + 2) * kRadix] = sh.aux[0][t];  // this thread's own column: no barrier needed
             col[(chunks + 3) * kRadix] = sh.aux[1][t];
@@ -1786,7 +1801,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
                 } else {
                     if (threadIdx.x == 0) {
                         runs_begin(lds.queue.emit);
-                        add_run(lds.queue.emit, record_run(q, b, mm, 0u, ~0u));
+                        add_run(lds.queue.emit, record_run(q, b, mm, 0u, false, 0u, 0u));
                     }
                     emit_jobs(q, lds.queue.emit);
                 }
@@ -1814,7 +1829,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
         }
         if (threadIdx.x == 0) {
             runs_begin(lds.queue.emit);
-            add_run(lds.queue.emit, record_run(q, begin, m, 0u, ~0u));
+            add_run(lds.queue.emit, record_run(q, begin, m, 0u, false, 0u, 0u));
         }
         emit_jobs(q, lds.queue.emit);
         return;
@@ -2042,38 +2057,38 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
             const uint64_t* sk = s.src ? alt_k : keys;
             uint32_t* col = q.pool + s.pool + t;  // this thread's digit column
             if (type == J_REDUCE) {
-                uint32_t a = 0xffffffffu, o = 0u;
+                uint32_t lo = 0xffffffffu, hi = 0u;
 #pragma unroll
                 for (int u = 0; u < kChunk / kBlock; u++) {
                     const uint32_t i = t + u * kBlock;
                     if (i < cnt) {
                         const uint32_t x = (uint32_t)sk[begin + c0 + i];
-                        a &= x;
-                        o |= x;
+                        lo = min(lo, x);
+                        hi = max(hi, x);
                     }
                 }
-                wave_and_or(a, o);
+                wave_min_max(lo, hi);
                 if (lane == 0) {
-                    s_and[wave] = a;
-                    s_or[wave] = o;
+                    s_and[wave] = lo;
+                    s_or[wave] = hi;
                 }
                 __syncthreads();
                 if (t == 0) {
                     for (int w = 0; w < kWavesPerBlock; w++) {
-                        a &= s_and[w];
-                        o |= s_or[w];
+                        lo = min(lo, s_and[w]);
+                        hi = max(hi, s_or[w]);
                     }
-                    __hip_atomic_fetch_and(&s.and_bits, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_or(&s.or_bits, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_min(&s.lo_bits, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_max(&s.hi_bits, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 if (finish_phase(s, &s_flag)) {
                     if (t == 0) {
                         runs_begin(e);
-                        const uint32_t diff = q_load(&s.and_bits) ^ q_load(&s.or_bits);
-                        if (diff == 0) {  // equal low keys: already in stable order
+                        const uint32_t rlo = q_load(&s.lo_bits), rhi = q_load(&s.hi_bits);
+                        if (rlo == rhi) {  // equal low keys: already in stable order
                             if (s.src) add_run(e, J_COPY, 1u, begin, m, chunks);
                         } else {
-                            set_digit(s, diff);
+                            set_digit(s, rlo, rhi);
                             s.pending = chunks;
                             add_run(e, J_HIST, 0u, job.y, 0u, chunks);
                         }
@@ -2083,7 +2098,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
             } else if (type == J_HIST) {
                 const int shift = (int)s.shift;
                 const uint32_t mask = (1u << s.bits) - 1u;
-                col[c * kRadix] = chunk_hist(sk, begin + c0, cnt, shift, mask, sh);
+                col[c * kRadix] = chunk_hist(sk, begin + c0, cnt, s.lo, shift, mask, sh);
                 if (finish_phase(s, &s_flag)) {
                     plan_scatter(col, chunks, begin, sh);
                     if (t == 0) {
@@ -2105,14 +2120,14 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                 sh.aux[1][t] = 0u;
                 for (uint32_t b0 = 0; b0 < cnt; b0 += kBigStep)
                     scatter_step<true>(sk, sv, dk, dv, begin + c0 + b0,
-                                       cnt - b0 < (uint32_t)kBigStep ? cnt - b0 : (uint32_t)kBigStep, shift, mask,
-                                       begin, begin + m, sh);
-                // this chunk's per-digit AND / OR into the record's (digits it holds only)
+                                       cnt - b0 < (uint32_t)kBigStep ? cnt - b0 : (uint32_t)kBigStep, s.lo, shift,
+                                       mask, begin, begin + m, sh);
+                // this chunk's per-digit MIN / MAX into the record's (digits it holds only)
                 if (sh.aux[0][t] != 0xffffffffu || sh.aux[1][t] != 0u) {
-                    __hip_atomic_fetch_and(&col[(chunks + 2) * kRadix], sh.aux[0][t], __ATOMIC_RELAXED,
+                    __hip_atomic_fetch_min(&col[(chunks + 2) * kRadix], sh.aux[0][t], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_or(&col[(chunks + 3) * kRadix], sh.aux[1][t], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_max(&col[(chunks + 3) * kRadix], sh.aux[1][t], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
                 }
                 if (finish_phase(s, &s_flag)) {
                     cut_pieces(q, e, sh, col, chunks, begin, m, shift, dst);

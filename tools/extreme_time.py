@@ -18,24 +18,36 @@ cases = {"uniform tiles": torch.randint(0, T, (n,), generator=g), "uniform, z 2-
          "two tiles": torch.where(torch.rand(n, generator=g) < 0.5, 5, 8000),
          "64 tiles": torch.randint(0, 64, (n,), generator=g) * 127}
 vals = torch.arange(n, dtype=torch.int32).cuda()
+from hidegs_amd import synthetic  # noqa: E402
+
+cam = synthetic.d2_camera(1920, 1080)
+for frac, rad in ((0.15, 0.1), (0.5, 0.02)):  # D2 hot-tile views with depths widened to [0.2, 100]
+    wl = synthetic.d2_binning_workload(synthetic.d2_scene(2_000_000, cam, seed=1000, cluster=(frac, rad)), cam)
+    zg = (torch.rand(2_000_000, generator=g) * 99.8 + 0.2).view(torch.int32).long() & 0xFFFFFFFF
+    cases[f"D2 {frac}:{rad} z.2-100"] = ((wl.keys >> 32) << 32) | zg[wl.values.long()]
 for name, tiles in cases.items():
-    if tiles is None:
+    if name.startswith("D2 "):
+        keys = tiles.cuda()
+        vals_c = torch.arange(keys.numel(), dtype=torch.int32).cuda()
+    elif tiles is None:
         keys = ((cases["uniform tiles"].long() << 32) | d2).cuda()
     else:
         keys = ((tiles.long() << 32) | depth).cuda()
+    if not name.startswith("D2 "):
+        vals_c = vals
     for _ in range(2):
-        primitives.sort_tile_pairs(keys, vals, T)
+        primitives.sort_tile_pairs(keys, vals_c, T)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(5):
-        primitives.sort_tile_pairs(keys, vals, T)
+        primitives.sort_tile_pairs(keys, vals_c, T)
     e1.record()
     torch.cuda.synchronize()
     with _lib.kernel_timer() as kt:
-        primitives.sort_tile_pairs(keys, vals, T)
+        primitives.sort_tile_pairs(keys, vals_c, T)
         torch.cuda.synchronize()
         per = {k: round(kt.get(k)[0] * 1e3, 1) for k in ("radix_hist_u64", "radix_digit_scan", "radix_scatter_u64",
                                                            "segment_sort", "big_segments")}
-    print(f"{name:14s} n={n}: sort {e0.elapsed_time(e1) * 1e3 / 5:8.1f} us  {per}  qerr {primitives.queue_error()}",
+    print(f"{name:14s} n={keys.numel()}: sort {e0.elapsed_time(e1) * 1e3 / 5:8.1f} us  {per}  qerr {primitives.queue_error()}",
           flush=True)
