@@ -242,8 +242,13 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
     end_bit = 32 + primitives.higher_msb(T)
     offsets = torch.empty_like(wl.tiles_touched)
     V = int((wl.tiles_touched > 0).sum())
-    line["config"].update({"tiles": T, "pairs_K": K, "visible_V": V, "pixels_Px": cam.width * cam.height,
-                           "sort_bits": [0, end_bit]})
+    Px = cam.width * cam.height
+    line["config"].update({"tiles": T, "pairs_K": K, "visible_V": V, "pixels_Px": Px,
+                           "sort_bits": [0, end_bit],
+                           # the fwd+bwd iteration's algorithmic bytes at this view (the
+                           # headline's denominator were the rasterizer built); the binning sort's share
+                           # of it is the 24 B/pair sort term
+                           "B_iter_bytes": 288 * N + 542 * V + 164 * K + 112 * Px + 24 * T})
 
     def make_step(w):
         off = torch.empty_like(w.tiles_touched)
