@@ -1025,18 +1025,56 @@ __device__ __forceinline__ uint32_t rec_digit(uint64_t key, uint32_t lo, int shi
     return (((uint32_t)key - lo) >> shift) & mask;
 }
 
+// Chunk groups of a big record.  The SCATTER phase needs, per chunk and digit, the digit's count in
+// the chunks before it: one workgroup walking the digit columns of all chunks took 246 us for a
+// 8.5M-pair record (2100 dependent rows).  A record of more than kGroupChunks chunks therefore
+// counts its HIST phase down per group: the last chunk of a group turns the group's counts into
+// prefixes within the group and its sum row, the last group plans the groups' bases (<= 256 rows).
+constexpr uint32_t kGroupChunks = 32;
+__device__ __forceinline__ uint32_t group_chunks(uint32_t chunks)
+{
+    const uint32_t g = (chunks + kRadix - 1) / kRadix;  // at most 256 groups
+    return g > kGroupChunks ? g : kGroupChunks;
+}
+__device__ __forceinline__ uint32_t num_groups(uint32_t chunks)  // 0: an ungrouped record
+{
+    return chunks > kGroupChunks ? (chunks + group_chunks(chunks) - 1) / group_chunks(chunks) : 0u;
+}
+// Pool rows of a record: [0, chunks) per-chunk counts -> destinations (grouped: prefixes within the
+// group), chunks + 0..3 the digit starts, totals, MIN and MAX, then (grouped) one row per group (its
+// sums -> its bases) and one row of group countdowns.
+__device__ __forceinline__ uint32_t pool_rows(uint32_t chunks)
+{
+    // num_groups(chunks) <= chunks / kGroupChunks + 1 (a bound without branches: the exact count
+    // here cost segment_sort_kernel, where the scouts open records, 4 spilled VGPRs)
+    return chunks + 4 + chunks / kGroupChunks + 2;
+}
+// One thread: a record's HIST countdown (chunks, or its groups with each group's own countdown);
+// the stores are published by the emit_jobs that queues the HIST jobs.
+__device__ __forceinline__ uint32_t hist_countdown(const BigQueue& q, const BigSeg& s)
+{
+    const uint32_t ng = num_groups(s.chunks);
+    if (ng == 0) return s.chunks;
+    const uint32_t G = group_chunks(s.chunks);
+    uint32_t* down = q.pool + s.pool + (s.chunks + 4 + ng) * kRadix;
+    for (uint32_t g = 0; g < ng; g++) down[g] = s.chunks - g * G < G ? s.chunks - g * G : G;
+    return ng;
+}
+
 // A new record over [begin, begin + m) of buffer src, as the run of jobs that starts it: REDUCE
 // chunk jobs, or -- when the low keys' range [lo, hi] is known already (from the parent's SCATTER or
 // the opener; `known` false: unknown) -- HIST chunk jobs right away, or a COPY / nothing for a piece
 // of equal low keys.  With the record table or the pool full: one GLOBAL job (the one-workgroup sort).
-// The pool holds (chunks + 4) x 256 u32: per-chunk counts -> destinations, then the digit starts,
-// totals, and MIN / MAX of each digit's low key halves (the next level's range).
+// The pool holds pool_rows(chunks) x 256 u32: per-chunk counts -> destinations, then the digit
+// starts, totals, and MIN / MAX of each digit's low key halves (the next level's range), and the
+// rows of the chunk groups.
+template <bool Grouped = true>  // false: the caller knows m <= kGroupChunks chunks (no countdowns)
 __device__ __forceinline__ uint4 record_run(const BigQueue& q, uint32_t begin, uint32_t m, uint32_t src,
                                             bool known, uint32_t lo, uint32_t hi)
 {
     const uint32_t chunks = (m + kChunk - 1) / kChunk;
     if (known && lo == hi) return make_uint4(J_COPY | (src << 8), begin, m, src ? chunks : 0u);  // already in order
-    const uint32_t need = (chunks + 4) * kRadix;
+    const uint32_t need = (Grouped ? pool_rows(chunks) : chunks + 4) * kRadix;
     const uint32_t r = __hip_atomic_fetch_add(&q.ctl[kCtlStride * Q_NREC], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t p = ~0u;
     if (r < q.rec_cap) {
@@ -1058,6 +1096,7 @@ __device__ __forceinline__ uint4 record_run(const BigQueue& q, uint32_t begin, u
     s.pending = chunks;
     if (!known) return make_uint4(J_REDUCE, r, 0u, chunks);
     set_digit(s, lo, hi);
+    if (Grouped) s.pending = hist_countdown(q, s);
     return make_uint4(J_HIST, r, 0u, chunks);
 }
 
@@ -1086,8 +1125,13 @@ __device__ __forceinline__ void emit_jobs(const BigQueue& q, EmitShared& e)
     const uint32_t base = e.base;
     if (base == ~0u) return;
     for (uint32_t j = t; j < total; j += kBlock) {
-        uint32_t r = 0;
-        while (e.off[r + 1] <= j) r++;
+        // the run holding job j: off[r] <= j < off[r + 1] (a binary search -- a linear walk over a
+        // split record's 256 runs cost its last SCATTER job ~60 us of dependent LDS reads)
+        uint32_t r = 0, hi = nr;
+        while (hi - r > 1u) {
+            const uint32_t mid = (r + hi) >> 1;
+            if (e.off[mid] <= j) r = mid; else hi = mid;
+        }
         q.job[base + j] = run_job(e.run[r], j - e.off[r]);  // tag (.w) 0: not yet published
     }
     wave_stores_done();  // the jobs (and record / pool / pair stores) before the publish below
@@ -1121,33 +1165,45 @@ __device__ __forceinline__ uint32_t chunk_hist(const uint64_t* sk, const uint32_
     return sh.hist[t];
 }
 
-// After every chunk's counts are in the record's pool (col = this thread's digit column): every
-// chunk's destination of each digit (begin + digit start + the digit's count in the chunks before
-// it), the digit starts and totals, and the MIN / MAX rows the SCATTER jobs gather into.
-__device__ __forceinline__ void plan_scatter(uint32_t* col, const uint32_t chunks, const uint32_t begin, BigShared& sh)
+// Rows [r0, r0 + n) of this thread's digit column: each count becomes base + the counts before it
+// (an exclusive scan down the column); returns the column's sum.
+__device__ __forceinline__ uint32_t scan_column(uint32_t* col, const uint32_t r0, const uint32_t n, uint32_t base)
 {
     constexpr uint32_t U = 8;  // independent loads in flight: the column is in other XCDs' writes
-    uint32_t tot = 0u;
-    for (uint32_t j0 = 0; j0 < chunks; j0 += U) {
+    for (uint32_t j0 = 0; j0 < n; j0 += U) {
         uint32_t x[U];
 #pragma unroll
-        for (uint32_t u = 0; u < U; u++) x[u] = j0 + u < chunks ? col[(j0 + u) * kRadix] : 0u;
+        for (uint32_t u = 0; u < U; u++) x[u] = j0 + u < n ? col[(r0 + j0 + u) * kRadix] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            if (j0 + u < n) col[(r0 + j0 + u) * kRadix] = base;
+            base += x[u];
+        }
+    }
+    return base;
+}
+
+// After every chunk's counts are in the record's pool (col = this thread's digit column) -- for a
+// grouped record, every group's sums (the chunks' rows hold prefixes within their group): every
+// chunk's (group's) destination of each digit (begin + digit start + the digit's count in the chunks
+// (groups) before it), the digit starts and totals, and the MIN / MAX rows the SCATTER jobs gather into.
+template <bool Grouped = true>  // false: the caller knows the record is ungrouped
+__device__ __forceinline__ void plan_scatter(uint32_t* col, const uint32_t chunks, const uint32_t begin, BigShared& sh)
+{
+    constexpr uint32_t U = 8;
+    const uint32_t ng = Grouped ? num_groups(chunks) : 0u;
+    const uint32_t r0 = ng ? chunks + 4 : 0u, n = ng ? ng : chunks;
+    uint32_t tot = 0u;
+    for (uint32_t j0 = 0; j0 < n; j0 += U) {
+        uint32_t x[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) x[u] = j0 + u < n ? col[(r0 + j0 + u) * kRadix] : 0u;
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) tot += x[u];
     }
     uint32_t dummy;
     const uint32_t start = block_exclusive_scan(tot, sh.wave, &dummy);
-    uint32_t run = begin + start;
-    for (uint32_t j0 = 0; j0 < chunks; j0 += U) {
-        uint32_t x[U];
-#pragma unroll
-        for (uint32_t u = 0; u < U; u++) x[u] = j0 + u < chunks ? col[(j0 + u) * kRadix] : 0u;
-#pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            if (j0 + u < chunks) col[(j0 + u) * kRadix] = run;
-            run += x[u];
-        }
-    }
+    scan_column(col, r0, n, begin + start);
     col[chunks * kRadix] = start;
     col[(chunks + 1) * kRadix] = tot;
     col[(chunks + 2) * kRadix] = 0xffffffffu;
@@ -1665,6 +1721,7 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
 #define HIDEGS_OPEN_LOCAL 24576
 #endif
 constexpr int kOpenLocal = HIDEGS_OPEN_LOCAL;
+static_assert(kOpenLocal <= (int)kGroupChunks * kChunk, "open_local plans an ungrouped record (pending == chunks)");
 #ifndef HIDEGS_SCATTER_LOCAL
 #define HIDEGS_SCATTER_LOCAL 0  // ... and up to this many, its SCATTER phase too (0: never; DESIGN.md, range digits)
 #endif
@@ -1709,7 +1766,7 @@ __device__ __forceinline__ void open_local(const uint64_t* keys, const uint32_t*
     if (lo == hi) return;  // equal low keys: in stable order already (block-uniform)
     if (t == 0) {
         runs_begin(e);
-        const uint4 r = record_run(q, begin, m, 0u, true, lo, hi);
+        const uint4 r = record_run<false>(q, begin, m, 0u, true, lo, hi);
         e.run[0] = r;
         e.base = (r.x & 0xffu) == J_HIST ? q.rec[r.y].pool : ~0u;
         if (e.base == ~0u) add_run(e, r);  // the table or pool is full: a GLOBAL job
@@ -1727,7 +1784,7 @@ __device__ __forceinline__ void open_local(const uint64_t* keys, const uint32_t*
                                          lo, shift, mask, sh);
         }
         __syncthreads();
-        plan_scatter(col, chunks, begin, sh);
+        plan_scatter<false>(col, chunks, begin, sh);
         if (m <= (uint32_t)kScatterLocal) {
             // and the SCATTER phase too: only the pieces go to the queue
             sh.aux[0][t] = 0xffffffffu;
@@ -1961,13 +2018,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
 }
 
 
-// The last workgroup to finish a phase job of record s goes on (returns true); the others return
-// false.  The caller's global writes are published before the count-down.
-__device__ __forceinline__ bool finish_phase(BigSeg& s, uint32_t* s_flag)
+// The last workgroup to count `pending` down (a record's phase, or a chunk group of its HIST phase)
+// goes on (returns true); the others return false.  The caller's global writes are published before
+// the count-down.
+__device__ __forceinline__ bool finish_phase(uint32_t& pending, uint32_t* s_flag)
 {
     wave_stores_done();
     __syncthreads();
-    if (threadIdx.x == 0) *s_flag = q_add(&s.pending, 0xffffffffu) == 1u;  // release + acquire
+    if (threadIdx.x == 0) *s_flag = q_add(&pending, 0xffffffffu) == 1u;  // release + acquire
     __syncthreads();
     return *s_flag != 0;
 }
@@ -2081,7 +2139,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                     __hip_atomic_fetch_min(&s.lo_bits, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_fetch_max(&s.hi_bits, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                if (finish_phase(s, &s_flag)) {
+                if (finish_phase(s.pending, &s_flag)) {
                     if (t == 0) {
                         runs_begin(e);
                         const uint32_t rlo = q_load(&s.lo_bits), rhi = q_load(&s.hi_bits);
@@ -2089,7 +2147,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                             if (s.src) add_run(e, J_COPY, 1u, begin, m, chunks);
                         } else {
                             set_digit(s, rlo, rhi);
-                            s.pending = chunks;
+                            s.pending = hist_countdown(q, s);
                             add_run(e, J_HIST, 0u, job.y, 0u, chunks);
                         }
                     }
@@ -2099,7 +2157,19 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                 const int shift = (int)s.shift;
                 const uint32_t mask = (1u << s.bits) - 1u;
                 col[c * kRadix] = chunk_hist(sk, begin + c0, cnt, s.lo, shift, mask, sh);
-                if (finish_phase(s, &s_flag)) {
+                const uint32_t ng = num_groups(chunks);
+                bool last;
+                if (ng) {  // the group's countdown first; its last chunk scans the group's rows
+                    const uint32_t G = group_chunks(chunks), g = c / G, g0 = g * G;
+                    last = finish_phase(q.pool[s.pool + (chunks + 4 + ng) * kRadix + g], &s_flag);
+                    if (last) {
+                        col[(chunks + 4 + g) * kRadix] = scan_column(col, g0, chunks - g0 < G ? chunks - g0 : G, 0u);
+                        last = finish_phase(s.pending, &s_flag);
+                    }
+                } else {
+                    last = finish_phase(s.pending, &s_flag);
+                }
+                if (last) {
                     plan_scatter(col, chunks, begin, sh);
                     if (t == 0) {
                         s.pending = chunks;
@@ -2115,7 +2185,8 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                 const uint32_t* sv = s.src ? alt_v : vals;
                 uint64_t* dk = dst ? alt_k : keys;
                 uint32_t* dv = dst ? alt_v : vals;
-                sh.run[t] = col[c * kRadix];
+                const uint32_t ng = num_groups(chunks);  // grouped: + the group's base
+                sh.run[t] = col[c * kRadix] + (ng ? col[(chunks + 4 + c / group_chunks(chunks)) * kRadix] : 0u);
                 sh.aux[0][t] = 0xffffffffu;
                 sh.aux[1][t] = 0u;
                 for (uint32_t b0 = 0; b0 < cnt; b0 += kBigStep)
@@ -2129,7 +2200,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                     __hip_atomic_fetch_max(&col[(chunks + 3) * kRadix], sh.aux[1][t], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
-                if (finish_phase(s, &s_flag)) {
+                if (finish_phase(s.pending, &s_flag)) {
                     cut_pieces(q, e, sh, col, chunks, begin, m, shift, dst);
                     emit_jobs(q, e);
                 }
@@ -2222,7 +2293,7 @@ constexpr long long kSegmentedMinAvg = 64;   // pairs per segment on average, el
 // records of one level are disjoint: <= n / 2049 per level, 5 levels (4 digits + the copy).  A
 // record queues <= 3 jobs per chunk of 4096 pairs and <= 2 pieces per kSegRun pairs (a piece lies in
 // one kSegRun window or is a digit of its own) -- under n / 39 jobs in all, so job_cap (n / 24,
-// zeroed every call: n / 1.5 bytes) cannot overflow.  The pool ((chunks + 4) x 256 u32 per record)
+// zeroed every call: n / 1.5 bytes) cannot overflow.  The pool (pool_rows(chunks) x 256 u32 per record)
 // is sized for a few hot tiles' worth; a record that finds it (or the record table) full is sorted
 // by one workgroup instead (a GLOBAL job) -- slower, same result.
 BigQueue queue_caps(long long n)

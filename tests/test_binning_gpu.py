@@ -566,3 +566,29 @@ def test_whole_input_in_one_or_two_tiles(case):
     assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
     assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
 
+
+def test_one_tile_of_36m_pairs_properties():
+    """One tile of 36M pairs: a record of 8790 chunks counted down in 252 groups of 35 (more than 256
+    groups of kGroupChunks would not fit its countdown row), whose digits of ~140K pairs are grouped
+    records again.  At a size the oracle is slow for, the result is checked by size-independent
+    properties: the output holds the input's pairs (keys[vo] == ko, vo a permutation), in key order
+    with equal keys in input order (float32 depths of 36M draws repeat), and one range spans it all."""
+    n, T = 36_000_000, 8160
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    depth = torch.empty(n, device="cuda").uniform_(0.2, 100.0, generator=gen)
+    keys = (torch.full((n,), 77, dtype=torch.int64, device="cuda") << 32) | depth.view(torch.int32).to(torch.int64)
+    del depth
+    vals = torch.arange(n, dtype=torch.int32, device="cuda")
+    ko, vo, r = primitives.sort_tile_pairs(keys, vals, T)
+    assert primitives.queue_error() == 0
+    assert torch.equal(keys[vo.long()], ko)
+    dk = ko[1:] - ko[:-1]  # one tile: no int64 overflow
+    assert bool((dk >= 0).all())
+    tie = dk == 0
+    assert int(tie.sum()) > 1000
+    assert bool((vo[1:][tie] > vo[:-1][tie]).all())
+    del dk, tie
+    assert torch.equal(torch.sort(vo).values, vals)
+    rr = r.cpu()
+    assert rr[77].tolist() == [0, n] and int((rr[:, 1] > rr[:, 0]).sum()) == 1
+
