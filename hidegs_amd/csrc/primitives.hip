@@ -884,7 +884,24 @@ static_assert(sizeof(BucketShared) >= kSegRun * (sizeof(uint64_t) + sizeof(uint3
 #ifndef HIDEGS_CHUNK_STEPS
 #define HIDEGS_CHUNK_STEPS 2
 #endif
-constexpr int kChunk = HIDEGS_CHUNK_STEPS * kBigStep;  // pairs per chunk job
+constexpr int kChunk = HIDEGS_CHUNK_STEPS * kBigStep;  // pairs per chunk job of a small record
+// A bigger record's chunk jobs take 2, 4 or 8 kChunk pieces each: a job's hand-off (claim, acquire,
+// release) costs ~10 us whatever its size, so the 2100 chunk jobs per phase of an 8.6M-pair tile
+// spent most of their time in hand-offs (tools/gpu_queue_ab.sh: DESIGN.md "A known limit").
+#ifndef HIDEGS_CHUNK_X2
+#define HIDEGS_CHUNK_X2 32768
+#endif
+#ifndef HIDEGS_CHUNK_X4
+#define HIDEGS_CHUNK_X4 131072
+#endif
+#ifndef HIDEGS_CHUNK_X8
+#define HIDEGS_CHUNK_X8 1048576
+#endif
+static_assert((kChunk & (kChunk - 1)) == 0, "chunk sizes are kChunk << 0..3");
+__device__ __forceinline__ uint32_t chunk_size(uint32_t m)
+{
+    return (uint32_t)kChunk << (m > HIDEGS_CHUNK_X8 ? 3 : m > HIDEGS_CHUNK_X4 ? 2 : m > HIDEGS_CHUNK_X2 ? 1 : 0);
+}
 #ifndef HIDEGS_QUEUE_BLOCKS
 #define HIDEGS_QUEUE_BLOCKS 256  // queue workers (experiments: tools/build_variant.py)
 #endif
@@ -919,7 +936,7 @@ struct BigSeg {
     uint32_t pool;                   // (chunks + 2) x 256 u32: per-chunk counts -> destinations,
                                      // then the digit starts and the digit totals
     uint32_t pending;                // jobs of the current phase not yet finished
-    uint32_t pad[1];
+    uint32_t csize;                  // pairs per chunk job (chunk_size(m))
 };
 
 struct BigQueue {
@@ -1072,8 +1089,10 @@ template <bool Grouped = true>  // false: the caller knows m <= kGroupChunks chu
 __device__ __forceinline__ uint4 record_run(const BigQueue& q, uint32_t begin, uint32_t m, uint32_t src,
                                             bool known, uint32_t lo, uint32_t hi)
 {
-    const uint32_t chunks = (m + kChunk - 1) / kChunk;
-    if (known && lo == hi) return make_uint4(J_COPY | (src << 8), begin, m, src ? chunks : 0u);  // already in order
+    if (known && lo == hi)  // already in order
+        return make_uint4(J_COPY | (src << 8), begin, m, src ? (m + kChunk - 1) / kChunk : 0u);
+    const uint32_t csize = Grouped ? chunk_size(m) : (uint32_t)kChunk;
+    const uint32_t chunks = (m + csize - 1) >> (31 - __builtin_clz(csize));
     const uint32_t need = (Grouped ? pool_rows(chunks) : chunks + 4) * kRadix;
     const uint32_t r = __hip_atomic_fetch_add(&q.ctl[kCtlStride * Q_NREC], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t p = ~0u;
@@ -1094,6 +1113,7 @@ __device__ __forceinline__ uint4 record_run(const BigQueue& q, uint32_t begin, u
     s.lo = 0u;
     s.pool = p;
     s.pending = chunks;
+    s.csize = csize;
     if (!known) return make_uint4(J_REDUCE, r, 0u, chunks);
     set_digit(s, lo, hi);
     if (Grouped) s.pending = hist_countdown(q, s);
@@ -1145,22 +1165,24 @@ __device__ __forceinline__ void emit_jobs(const BigQueue& q, EmitShared& e)
         __hip_atomic_store(&q.job[base + j].w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Thread t's result: the number of the cnt <= kChunk keys at sk[base..] whose digit is t.
+// Thread t's result: the number of the cnt keys at sk[base..] whose digit is t (kChunk at a time).
 __device__ __forceinline__ uint32_t chunk_hist(const uint64_t* sk, const uint32_t base, const uint32_t cnt,
                                                const uint32_t lo, const int shift, const uint32_t mask, BigShared& sh)
 {
     const int t = threadIdx.x;
     sh.hist[t] = 0u;
     __syncthreads();
-    uint32_t dg[kChunk / kBlock];
+    for (uint32_t i0 = 0; i0 < cnt; i0 += kChunk) {
+        uint32_t dg[kChunk / kBlock];
 #pragma unroll
-    for (int u = 0; u < kChunk / kBlock; u++) {
-        const uint32_t i = t + u * kBlock;
-        dg[u] = i < cnt ? rec_digit(sk[base + i], lo, shift, mask) : ~0u;
+        for (int u = 0; u < kChunk / kBlock; u++) {
+            const uint32_t i = i0 + t + u * kBlock;
+            dg[u] = i < cnt ? rec_digit(sk[base + i], lo, shift, mask) : ~0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kChunk / kBlock; u++)
+            if (dg[u] != ~0u) atomicAdd(&sh.hist[dg[u]], 1u);
     }
-#pragma unroll
-    for (int u = 0; u < kChunk / kBlock; u++)
-        if (dg[u] != ~0u) atomicAdd(&sh.hist[dg[u]], 1u);
     __syncthreads();
     return sh.hist[t];
 }
@@ -1231,7 +1253,7 @@ __device__ __forceinline__ void cut_pieces(const BigQueue& q, EmitShared& e, Big
     if (shift == 0) {  // every varying bit is placed: the record is sorted
         if (t == 0) {
             runs_begin(e);
-            if (dst) add_run(e, J_COPY, 1u, begin, m, chunks);
+            if (dst) add_run(e, J_COPY, 1u, begin, m, (m + kChunk - 1) / kChunk);  // kChunk pieces
         }
     } else {
         const bool nonempty = n_d != 0u, solo = n_d > (uint32_t)kSegRun;
@@ -2110,19 +2132,21 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
             segment_sort_global(keys, vals, alt_k, alt_v, job.y, job.z, sh);
         } else {  // a chunk job of record job.y
             BigSeg& s = q.rec[job.y];
-            const uint32_t c = job.z, begin = s.begin, m = s.m, chunks = s.chunks;
-            const uint32_t c0 = c * kChunk, cnt = m - c0 < (uint32_t)kChunk ? m - c0 : (uint32_t)kChunk;
+            const uint32_t c = job.z, begin = s.begin, m = s.m, chunks = s.chunks, csize = s.csize;
+            const uint32_t c0 = c * csize, cnt = m - c0 < csize ? m - c0 : csize;
             const uint64_t* sk = s.src ? alt_k : keys;
             uint32_t* col = q.pool + s.pool + t;  // this thread's digit column
             if (type == J_REDUCE) {
                 uint32_t lo = 0xffffffffu, hi = 0u;
+                for (uint32_t i0 = 0; i0 < cnt; i0 += kChunk) {
 #pragma unroll
-                for (int u = 0; u < kChunk / kBlock; u++) {
-                    const uint32_t i = t + u * kBlock;
-                    if (i < cnt) {
-                        const uint32_t x = (uint32_t)sk[begin + c0 + i];
-                        lo = min(lo, x);
-                        hi = max(hi, x);
+                    for (int u = 0; u < kChunk / kBlock; u++) {
+                        const uint32_t i = i0 + t + u * kBlock;
+                        if (i < cnt) {
+                            const uint32_t x = (uint32_t)sk[begin + c0 + i];
+                            lo = min(lo, x);
+                            hi = max(hi, x);
+                        }
                     }
                 }
                 wave_min_max(lo, hi);
@@ -2144,7 +2168,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                         runs_begin(e);
                         const uint32_t rlo = q_load(&s.lo_bits), rhi = q_load(&s.hi_bits);
                         if (rlo == rhi) {  // equal low keys: already in stable order
-                            if (s.src) add_run(e, J_COPY, 1u, begin, m, chunks);
+                            if (s.src) add_run(e, J_COPY, 1u, begin, m, (m + kChunk - 1) / kChunk);
                         } else {
                             set_digit(s, rlo, rhi);
                             s.pending = hist_countdown(q, s);
