@@ -960,10 +960,6 @@ __device__ unsigned int g_wtrace_n;
 #else
 #define WSTAMP(k) do { } while (0)
 #endif
-__device__ __forceinline__ uint32_t q_add(uint32_t* p, uint32_t v)
-{
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ uint32_t q_load(uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
 // polling reads: coherent but without the acquire's cache invalidation (taken once, after the wait)
 __device__ __forceinline__ uint32_t q_peek(uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -974,6 +970,23 @@ __device__ __forceinline__ void fence_release() { __builtin_amdgcn_fence(__ATOMI
 // tile ran 1.2 ms): each wave only waits for its own stores to be acknowledged, then after a barrier
 // ONE thread's agent-scope release (L2 writeback) or acquire (invalidate) acts for the workgroup.
 __device__ __forceinline__ void wave_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// ONE lane's release for its workgroup (after every storing wave's wave_stores_done and a barrier),
+// before the flag, tag or count that publishes the stores.  The explicit wait after the L2 writeback
+// is not redundant: ROCm 7.2 drops the compiler's own wait after `buffer_wbl2` when it thinks the
+// wave has nothing outstanding, and the count then overtakes the write-back (a group countdown built
+// that way let a reader on another XCD scan stale count rows: an illegal address under load).
+__device__ __forceinline__ void release_lane()
+{
+    fence_release();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// ONE lane's acquire for its workgroup, after its relaxed poll matched or its countdown came last;
+// the wait completes the L1 invalidate before the barrier that lets the other waves load.
+__device__ __forceinline__ void acquire_lane()
+{
+    fence_acquire();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 // Sticky per-device copy of every queue error (bit 1: job slots exhausted, bit 4: a worker gave up
 // waiting), read and cleared by hidegs_queue_error(); the debug mode (hidegs_set_debug) checks it after
 // every sort.  A set bit means the sort's output is not trustworthy.
@@ -1156,7 +1169,7 @@ __device__ __forceinline__ void emit_jobs(const BigQueue& q, EmitShared& e)
     }
     wave_stores_done();  // the jobs (and record / pool / pair stores) before the publish below
     __syncthreads();
-    if (t == 0) fence_release();  // one L2 writeback for the workgroup (see wave_stores_done)
+    if (t == 0) release_lane();  // one L2 writeback for the workgroup (see wave_stores_done)
     __syncthreads();
     // publish: each slot's tag becomes 1 (slots publish independently -- a global publication
     // order would chain every producer behind the one that reserved before it: 80 records of one
@@ -2047,7 +2060,12 @@ __device__ __forceinline__ bool finish_phase(uint32_t& pending, uint32_t* s_flag
 {
     wave_stores_done();
     __syncthreads();
-    if (threadIdx.x == 0) *s_flag = q_add(&pending, 0xffffffffu) == 1u;  // release + acquire
+    if (threadIdx.x == 0) {
+        release_lane();
+        const bool last = __hip_atomic_fetch_add(&pending, 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
+        if (last) acquire_lane();
+        *s_flag = last;
+    }
     __syncthreads();
     return *s_flag != 0;
 }
@@ -2076,7 +2094,10 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
     for (;;) {
         __syncthreads();  // the previous job's LDS use is over
         if (t == 0) {
-            const uint32_t i = q_add(&q.ctl[kCtlStride * Q_HEAD], 1u);
+            // the claim only hands out a slot index: relaxed (an acq_rel RMW here is an L2 writeback
+            // and invalidate per job; the job's data is acquired after its tag is seen)
+            const uint32_t i = __hip_atomic_fetch_add(&q.ctl[kCtlStride * Q_HEAD], 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
 #ifdef HIDEGS_QUEUE_TRACE
             t_claim = wall_clock64();
             t_index = i;
@@ -2085,7 +2106,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
             uint32_t polls = 0, backoff = 1;
             for (; polls < kMaxPolls; polls++) {
                 if (i < q.job_cap && q_peek(&q.job[i].w) != 0u) {
-                    fence_acquire();  // for the whole workgroup (see wave_stores_done)
+                    acquire_lane();  // for the whole workgroup (see wave_stores_done)
                     job = q.job[i];
                     break;
                 }
