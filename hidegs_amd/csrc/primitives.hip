@@ -598,30 +598,37 @@ struct BigShared {
 // never, for consistent offsets -- a guard, not a case.
 constexpr int kBigItems = 8;
 constexpr int kBigStep = kBigItems * kBlock;  // 2048
+// A step's pairs in registers: wave w's items [w * 512, w * 512 + 512) of [base, base + cnt), in
+// (round, lane) order; absent items read as 0.
+__device__ __forceinline__ void step_load(const uint64_t* sk, const uint32_t* sv, const uint32_t base,
+                                          const uint32_t cnt, uint64_t (&k)[kBigItems], uint32_t (&v)[kBigItems])
+{
+    const uint32_t w0 = (threadIdx.x / kWave) * (kBigItems * kWave);
+#pragma unroll
+    for (int q = 0; q < kBigItems; q++) {
+        const uint32_t i = w0 + q * kWave + lane_id();
+        k[q] = i < cnt ? sk[base + i] : 0ull;
+        v[q] = i < cnt ? sv[base + i] : 0u;
+    }
+}
+
 // Track: also fold each item's low key half into sh.aux[0][digit] (MIN) and sh.aux[1][digit] (MAX).
 template <bool Track = false>
-__device__ __forceinline__ void scatter_step(const uint64_t* sk, const uint32_t* sv, uint64_t* dk, uint32_t* dv,
-                                             const uint32_t base, const uint32_t cnt, const uint32_t dbase,
-                                             const int shift, const uint32_t mask, const uint32_t lo,
-                                             const uint32_t hi, BigShared& sh)
+__device__ __forceinline__ void step_scatter(const uint64_t (&k)[kBigItems], const uint32_t (&v)[kBigItems],
+                                             const uint32_t base, const uint32_t cnt, uint64_t* dk, uint32_t* dv,
+                                             const uint32_t dbase, const int shift, const uint32_t mask,
+                                             const uint32_t lo, const uint32_t hi, BigShared& sh)
 {
     const int t = threadIdx.x;
     const int lane = lane_id();
     const int wave = t / kWave;
     for (int i = t; i < kWavesPerBlock * kRadix; i += kBlock) (&sh.cnt[0][0])[i] = 0;
     __syncthreads();
-    uint64_t k[kBigItems];
-    uint32_t v[kBigItems];
     bool ok[kBigItems];
     uint32_t rank[kBigItems];
     const uint32_t w0 = wave * (kBigItems * kWave);
 #pragma unroll
-    for (int q = 0; q < kBigItems; q++) {
-        const uint32_t i = w0 + q * kWave + lane;
-        ok[q] = i < cnt;
-        k[q] = ok[q] ? sk[base + i] : 0ull;
-        v[q] = ok[q] ? sv[base + i] : 0u;
-    }
+    for (int q = 0; q < kBigItems; q++) ok[q] = w0 + q * kWave + lane < cnt;
     wave_rank<uint64_t, kBigItems, true>(k, ok, shift, mask, sh.cnt[wave], rank, mask, dbase);
     __syncthreads();
     const uint32_t tot = digit_wave_prefix(sh.cnt);
@@ -635,6 +642,7 @@ __device__ __forceinline__ void scatter_step(const uint64_t* sk, const uint32_t*
             (void)rank;
 #else
             const uint32_t dst = sh.run[dd] + sh.cnt[wave][dd] + rank[q];
+            (void)base;
 #endif
             if (dst >= lo && dst < hi) {
                 dk[dst] = k[q];
@@ -651,6 +659,43 @@ __device__ __forceinline__ void scatter_step(const uint64_t* sk, const uint32_t*
     __syncthreads();
     sh.run[threadIdx.x] += tot;
     __syncthreads();
+}
+
+template <bool Track = false>
+__device__ __forceinline__ void scatter_step(const uint64_t* sk, const uint32_t* sv, uint64_t* dk, uint32_t* dv,
+                                             const uint32_t base, const uint32_t cnt, const uint32_t dbase,
+                                             const int shift, const uint32_t mask, const uint32_t lo,
+                                             const uint32_t hi, BigShared& sh)
+{
+    uint64_t k[kBigItems];
+    uint32_t v[kBigItems];
+    step_load(sk, sv, base, cnt, k, v);
+    step_scatter<Track>(k, v, base, cnt, dk, dv, dbase, shift, mask, lo, hi, sh);
+}
+
+// scatter_step over [base, base + cnt) in kBigStep steps, the next step's pairs loaded while the
+// current one is ranked and stored (the queue's workers run one wave per SIMD: latency is hidden
+// by the wave's own loads in flight or not at all; barriers do not wait for global loads).
+template <bool Track = false>
+__device__ __forceinline__ void scatter_steps(const uint64_t* sk, const uint32_t* sv, uint64_t* dk, uint32_t* dv,
+                                              const uint32_t base, const uint32_t cnt, const uint32_t dbase,
+                                              const int shift, const uint32_t mask, const uint32_t lo,
+                                              const uint32_t hi, BigShared& sh)
+{
+    uint64_t k[kBigItems], kn[kBigItems];
+    uint32_t v[kBigItems], vn[kBigItems];
+    step_load(sk, sv, base, cnt < (uint32_t)kBigStep ? cnt : (uint32_t)kBigStep, k, v);
+    for (uint32_t b0 = 0; b0 < cnt; b0 += kBigStep) {
+        const uint32_t c = cnt - b0 < (uint32_t)kBigStep ? cnt - b0 : (uint32_t)kBigStep;
+        const uint32_t b1 = b0 + kBigStep;
+        if (b1 < cnt) step_load(sk, sv, base + b1, cnt - b1 < (uint32_t)kBigStep ? cnt - b1 : (uint32_t)kBigStep, kn, vn);
+        step_scatter<Track>(k, v, base + b0, c, dk, dv, dbase, shift, mask, lo, hi, sh);
+#pragma unroll
+        for (int q = 0; q < kBigItems; q++) {
+            k[q] = kn[q];
+            v[q] = vn[q];
+        }
+    }
 }
 
 // A segment of more than kSegCap pairs sorted by ONE workgroup: 4 stable LSD passes over the low
@@ -1178,22 +1223,26 @@ __device__ __forceinline__ void emit_jobs(const BigQueue& q, EmitShared& e)
         __hip_atomic_store(&q.job[base + j].w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Thread t's result: the number of the cnt keys at sk[base..] whose digit is t (kChunk at a time).
+// Thread t's result: the number of the cnt keys at sk[base..] whose digit is t (U x kChunk keys
+// loaded at a time: the queue's workers, one wave per SIMD, take U = 4; open_local, inside
+// segment_sort_kernel's 72-VGPR budget, 1).
+constexpr int kQueueIlp = 4;
+template <int U = 1>
 __device__ __forceinline__ uint32_t chunk_hist(const uint64_t* sk, const uint32_t base, const uint32_t cnt,
                                                const uint32_t lo, const int shift, const uint32_t mask, BigShared& sh)
 {
     const int t = threadIdx.x;
     sh.hist[t] = 0u;
     __syncthreads();
-    for (uint32_t i0 = 0; i0 < cnt; i0 += kChunk) {
-        uint32_t dg[kChunk / kBlock];
+    for (uint32_t i0 = 0; i0 < cnt; i0 += U * kChunk) {
+        uint32_t dg[U * kChunk / kBlock];
 #pragma unroll
-        for (int u = 0; u < kChunk / kBlock; u++) {
+        for (int u = 0; u < U * kChunk / kBlock; u++) {
             const uint32_t i = i0 + t + u * kBlock;
             dg[u] = i < cnt ? rec_digit(sk[base + i], lo, shift, mask) : ~0u;
         }
 #pragma unroll
-        for (int u = 0; u < kChunk / kBlock; u++)
+        for (int u = 0; u < U * kChunk / kBlock; u++)
             if (dg[u] != ~0u) atomicAdd(&sh.hist[dg[u]], 1u);
     }
     __syncthreads();
@@ -2159,15 +2208,18 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
             uint32_t* col = q.pool + s.pool + t;  // this thread's digit column
             if (type == J_REDUCE) {
                 uint32_t lo = 0xffffffffu, hi = 0u;
-                for (uint32_t i0 = 0; i0 < cnt; i0 += kChunk) {
+                for (uint32_t i0 = 0; i0 < cnt; i0 += kQueueIlp * kChunk) {
+                    uint32_t x[kQueueIlp * kChunk / kBlock];
 #pragma unroll
-                    for (int u = 0; u < kChunk / kBlock; u++) {
+                    for (int u = 0; u < kQueueIlp * kChunk / kBlock; u++) {
                         const uint32_t i = i0 + t + u * kBlock;
-                        if (i < cnt) {
-                            const uint32_t x = (uint32_t)sk[begin + c0 + i];
-                            lo = min(lo, x);
-                            hi = max(hi, x);
-                        }
+                        x[u] = i < cnt ? (uint32_t)sk[begin + c0 + i] : 0xffffffffu;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kQueueIlp * kChunk / kBlock; u++) {
+                        const uint32_t i = i0 + t + u * kBlock;
+                        lo = min(lo, x[u]);
+                        hi = i < cnt ? max(hi, x[u]) : hi;
                     }
                 }
                 wave_min_max(lo, hi);
@@ -2201,7 +2253,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
             } else if (type == J_HIST) {
                 const int shift = (int)s.shift;
                 const uint32_t mask = (1u << s.bits) - 1u;
-                col[c * kRadix] = chunk_hist(sk, begin + c0, cnt, s.lo, shift, mask, sh);
+                col[c * kRadix] = chunk_hist<kQueueIlp>(sk, begin + c0, cnt, s.lo, shift, mask, sh);
                 const uint32_t ng = num_groups(chunks);
                 bool last;
                 if (ng) {  // the group's countdown first; its last chunk scans the group's rows
@@ -2234,10 +2286,7 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
                 sh.run[t] = col[c * kRadix] + (ng ? col[(chunks + 4 + c / group_chunks(chunks)) * kRadix] : 0u);
                 sh.aux[0][t] = 0xffffffffu;
                 sh.aux[1][t] = 0u;
-                for (uint32_t b0 = 0; b0 < cnt; b0 += kBigStep)
-                    scatter_step<true>(sk, sv, dk, dv, begin + c0 + b0,
-                                       cnt - b0 < (uint32_t)kBigStep ? cnt - b0 : (uint32_t)kBigStep, s.lo, shift,
-                                       mask, begin, begin + m, sh);
+                scatter_steps<true>(sk, sv, dk, dv, begin + c0, cnt, s.lo, shift, mask, begin, begin + m, sh);
                 // this chunk's per-digit MIN / MAX into the record's (digits it holds only)
                 if (sh.aux[0][t] != 0xffffffffu || sh.aux[1][t] != 0u) {
                     __hip_atomic_fetch_min(&col[(chunks + 2) * kRadix], sh.aux[0][t], __ATOMIC_RELAXED,
