@@ -907,10 +907,13 @@ static_assert(sizeof(BucketShared) >= kSegRun * (sizeof(uint64_t) + sizeof(uint3
 //
 // A segment of more than kSegCap pairs is not sorted by one workgroup (that costs ~10 ns per pair:
 // a 100K-pair tile took 1 ms) but split among many.  It becomes a RECORD, partitioned stably by
-// one digit -- its top <= 8 varying low-key bits -- in three phases of chunk jobs (kChunk pairs):
+// one digit -- the top <= 8 bits of (low key half - its MIN) -- in three phases of chunk jobs
+// (chunk_size(m) pairs: 4K to 32K by the record's size):
 //   REDUCE   MIN / MAX of the chunk's low key halves       -> the digit (last chunk decides)
-//   HIST     the chunk's digit counts                      -> pool; the last chunk scans them into
-//                                                             every chunk's per-digit destinations
+//   HIST     the chunk's digit counts                      -> pool; the last chunk (of each group
+//                                                             of chunks, then of the groups) scans
+//                                                             them into every chunk's per-digit
+//                                                             destinations
 //   SCATTER  the chunk's pairs, ranked stably, to the other buffer (keys <-> alt)
 // and the last SCATTER cuts the result into pieces by digit: runs of small digits merged up to
 // kSegCap pairs become SMALL jobs (the bucket form of segment_sort_kernel, alt -> keys or in place),
@@ -918,14 +921,14 @@ static_assert(sizeof(BucketShared) >= kSegRun * (sizeof(uint64_t) + sizeof(uint3
 // varying bits, so the chain ends within 4 levels; pieces left in alt are copied back (COPY jobs).
 // Every piece keeps its pairs in input order between equal digits, so the whole is the stable sort.
 //
-// Jobs live in a queue in scratch, zeroed each call: a producer reserves slots (CAS on `reserve`),
-// writes them and publishes each by setting its tag; a consumer workgroup claims the next index
-// (`head`) and waits until that slot is published or every job is finished (`done` == `reserve`:
+// Jobs live in a queue in scratch, zeroed each call: a producer reserves slots (fetch-add on
+// `reserve`), writes them and publishes each by setting its tag; a consumer workgroup claims the next
+// index (`head`, relaxed) and waits until that slot is published or every job is finished (`done` == `reserve`:
 // nothing in flight, so nothing more can come).  Every wait is bounded (kMaxPolls) and flags
 // Q_ERROR when exceeded.  Producers run (they reserved while resident) and publish right after
 // writing, so no wait is on a workgroup that is not running.  Ordering across workgroups (and XCD
-// L2s) is by agent-scope release / acquire: job payload and pair data before the tag, phase data
-// before `pending`.
+// L2s) is by agent-scope release / acquire (release_lane / acquire_lane): job payload and pair data
+// before the tag, phase data before `pending` and the group countdowns.
 #ifndef HIDEGS_CHUNK_STEPS
 #define HIDEGS_CHUNK_STEPS 2
 #endif
@@ -2385,7 +2388,7 @@ constexpr long long kSegmentedMinAvg = 64;   // pairs per segment on average, el
 
 // Capacities of the partition queue for n pairs.  Every record holds > kSegCap pairs and the
 // records of one level are disjoint: <= n / 2049 per level, 5 levels (4 digits + the copy).  A
-// record queues <= 3 jobs per chunk of 4096 pairs and <= 2 pieces per kSegRun pairs (a piece lies in
+// record queues <= 3 jobs per chunk of >= 4096 pairs and <= 2 pieces per kSegRun pairs (a piece lies in
 // one kSegRun window or is a digit of its own) -- under n / 39 jobs in all, so job_cap (n / 24,
 // zeroed every call: n / 1.5 bytes) cannot overflow.  The pool (pool_rows(chunks) x 256 u32 per record)
 // is sized for a few hot tiles' worth; a record that finds it (or the record table) full is sorted
