@@ -592,3 +592,37 @@ def test_one_tile_of_36m_pairs_properties():
     rr = r.cpu()
     assert rr[77].tolist() == [0, n] and int((rr[:, 1] > rr[:, 0]).sum()) == 1
 
+
+
+@pytest.mark.parametrize("case", ["d2_0.5_0.02", "one_tile_4m"])
+def test_queue_hand_offs_under_concurrent_load(case):
+    """The partition queue's hand-offs (tags, countdowns, group countdowns) under UNEVEN load: the same
+    sort repeated while large matrix products run on a second stream take CUs away from the queue's
+    workers at varying moments.  Every repetition must equal torch's stable sort of the same keys (equal
+    keys keep input order), with the queue's error word clear."""
+    from hidegs_amd import synthetic
+    if case == "one_tile_4m":
+        g = torch.Generator(device="cuda").manual_seed(9)
+        n, T = 4_000_000, 8160
+        depth = torch.empty(n, device="cuda").uniform_(0.2, 100.0, generator=g)
+        keys = (torch.full((n,), 4000, dtype=torch.int64, device="cuda") << 32) | depth.view(torch.int32).to(torch.int64)
+        vals = torch.arange(n, dtype=torch.int32, device="cuda")
+    else:
+        cam = synthetic.d2_camera(1920, 1080)
+        wl = synthetic.d2_binning_workload(synthetic.d2_scene(2_000_000, cam, seed=1000, cluster=(0.5, 0.02)), cam,
+                                           device="cuda")
+        keys, vals, T = wl.keys, wl.values, wl.num_tiles
+    _, perm = torch.sort(keys, stable=True)
+    ek, ev = keys[perm], vals[perm]
+    a = torch.randn(4096, 4096, device="cuda")
+    side = torch.cuda.Stream()
+    primitives.queue_error()
+    for it in range(6):
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(1 + it % 3):
+                a = torch.tanh(a @ a * 1e-3)
+        ko, vo, _ = primitives.sort_tile_pairs(keys, vals, T)
+        torch.cuda.synchronize()
+        assert torch.equal(ko, ek) and torch.equal(vo, ev), f"repetition {it}"
+        assert primitives.queue_error() == 0
