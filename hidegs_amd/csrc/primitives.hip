@@ -613,6 +613,8 @@ __device__ __forceinline__ void step_load(const uint64_t* sk, const uint32_t* sv
 }
 
 // Track: also fold each item's low key half into sh.aux[0][digit] (MIN) and sh.aux[1][digit] (MAX).
+// (Write-through `sc1` stores here, so that the SCATTER job's release had fewer dirty lines to write
+// back, measured slower: one tile 1044 -> 1188 us, D2 0.5:0.02 516 -> 547 us.)
 template <bool Track = false>
 __device__ __forceinline__ void step_scatter(const uint64_t (&k)[kBigItems], const uint32_t (&v)[kBigItems],
                                              const uint32_t base, const uint32_t cnt, uint64_t* dk, uint32_t* dv,
@@ -2156,17 +2158,24 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
 #endif
             uint4 job = make_uint4(J_EXIT, 0u, 0u, 0u);
             uint32_t polls = 0, backoff = 1;
+            bool reserved = false;  // slot i is reserved: a job will be published there (reserve only grows)
             for (; polls < kMaxPolls; polls++) {
                 if (i < q.job_cap && q_peek(&q.job[i].w) != 0u) {
                     acquire_lane();  // for the whole workgroup (see wave_stores_done)
                     job = q.job[i];
                     break;
                 }
-                if (q_peek(&q.ctl[kCtlStride * Q_DONE]) == q_peek(&q.ctl[kCtlStride * Q_RESERVE])) {
-                    // confirm in order: `done` (acquire) before `reserve`
-                    const uint32_t d = q_load(&q.ctl[kCtlStride * Q_DONE]);
-                    const uint32_t r = q_load(&q.ctl[kCtlStride * Q_RESERVE]);
-                    if (d == r && i >= r) break;  // nothing queued, nothing in flight: the end
+                // the shared counters are polled only while slot i is not reserved (reading `done` on
+                // one poll in 4 only, or backing off to 64 sleeps, measured slower: DESIGN.md)
+                if (!reserved) {
+                    const uint32_t r0 = q_peek(&q.ctl[kCtlStride * Q_RESERVE]);
+                    reserved = i < r0 && i < q.job_cap;
+                    if (!reserved && q_peek(&q.ctl[kCtlStride * Q_DONE]) == r0) {
+                        // confirm in order: `done` (acquire) before `reserve`
+                        const uint32_t d = q_load(&q.ctl[kCtlStride * Q_DONE]);
+                        const uint32_t r = q_load(&q.ctl[kCtlStride * Q_RESERVE]);
+                        if (d == r && i >= r) break;  // nothing queued, nothing in flight: the end
+                    }
                 }
                 for (uint32_t k = 0; k < backoff; k++) __builtin_amdgcn_s_sleep(8);  // ~0.2 us each
                 backoff = backoff < (uint32_t)HIDEGS_BACKOFF_MAX ? 2u * backoff : (uint32_t)HIDEGS_BACKOFF_MAX;
