@@ -437,6 +437,15 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
             "busbw_GBps": None if algbw is None else algbw * 2 * (world - 1) / world,
             "collectives_per_step": ex.last.collectives, "compacted": ex.last.compacted,
             "union_rows": ex.last.union_rows}
+        if world == 1 and gpu:
+            # the N-rank path forced on the one-rank group: every collective the multi-GPU run issues,
+            # real RCCL calls (over one rank a copy), so the machinery's own cost is on the record
+            exf = ViewDPExchange(transport=transport, force_collectives=True)
+            f_ms, _ = timed(lambda: exf.exchange(arena, visible, max_stats=[norm, radii]), reps, 2)
+            line["exchange" if transport == "fp32" else "exchange_bf16"]["forced_one_rank_rccl"] = {
+                "ms_per_step": round(f_ms, 3), "collectives_per_step": exf.last.collectives,
+                "wire_bytes": exf.last.wire_bytes, "compacted": exf.last.compacted,
+                "union_rows": exf.last.union_rows}
     st = ctx.get("adam_state")
     if st is not None:
         prm, opt, vis, g2 = st

@@ -69,6 +69,9 @@ SIGNATURES = {
     "hidegs_masked_adam": (I, [P, P, P, P, P, LL, I, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                                 LL, P]),
     "hidegs_masked_adam_multi": (I, [P, I, P]),
+    "hidegs_bf16_pack": (I, [P, P, LL, LL, P]),
+    "hidegs_bf16_sum_ranks": (I, [P, I, LL, P, P]),
+    "hidegs_bf16_unpack": (I, [P, P, LL, P]),
     "hidegs_kernel_timing": (None, [I]),
     "hidegs_kernel_timing_reset": (None, []),
     "hidegs_kernel_time": (I, [C.c_char_p, P, P]),

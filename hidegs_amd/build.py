@@ -25,7 +25,7 @@ INCLUDE = os.path.join(HERE, "..", "include")
 OBJDIR = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libhidegs.so")
 VARIANT_DIR = os.path.join(HERE, "variants")
-SOURCES = ["abi.cpp", "timing.cpp", "primitives.hip", "knn.hip", "adam.hip"]
+SOURCES = ["abi.cpp", "timing.cpp", "primitives.hip", "knn.hip", "adam.hip", "wire.hip"]
 HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "block_scan.h"), os.path.join(INCLUDE, "hidegs.h")]
 
 # -ffp-contract=off: every fused multiply-add in the kernels is an explicit fmaf, so the

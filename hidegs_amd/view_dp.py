@@ -53,6 +53,8 @@ from typing import Dict, Iterable, List, Optional, Union
 import torch
 import torch.distributed as dist
 
+from . import wire
+
 LEAF_WIDTHS = {"xyz": 3, "f_dc": 3, "f_rest": 45, "opacity": 1, "scaling": 3, "rotation": 4}
 """Per-Gaussian fp32 widths of the HiDeGS leaf parameters (59 floats = 236 B; SURVEY §8(e) E1)."""
 
@@ -158,8 +160,12 @@ class _Bucket:
             return 1
         n, w = self.view.numel(), self.world
         self.chunk = -(-n // (8 * w)) * 8  # 16-byte aligned chunks, one per rank
-        send = torch.zeros(self.chunk * w, dtype=torch.bfloat16, device=self.view.device)
-        send[:n].copy_(self.view.reshape(-1))  # round to nearest even
+        flat = self.view.reshape(-1)
+        if flat.is_cuda:  # one pass: round to nearest even, zero padding (csrc/wire.hip)
+            send = wire.bf16_pack(flat, torch.empty(self.chunk * w, dtype=torch.bfloat16, device=flat.device))
+        else:  # gloo ranks on the CPU: the definition as torch ops
+            send = torch.zeros(self.chunk * w, dtype=torch.bfloat16)
+            send[:n].copy_(flat)  # round to nearest even
         self.recv = torch.empty_like(send)
         # bf16 moved as bytes: the collective only moves them (gloo has no 16-bit all-to-all)
         self.work = dist.all_to_all_single(self.recv.view(torch.uint8), send.view(torch.uint8), group=self.group,
@@ -172,10 +178,13 @@ class _Bucket:
             return 0
         self.work.wait()
         parts = self.recv.view(self.world, self.chunk)
-        acc = parts[0].to(torch.float32)
-        for r in range(1, self.world):  # fp32, rank order: the same sum on whichever rank owns the chunk
-            acc += parts[r].to(torch.float32)
-        mine = acc.to(torch.bfloat16)
+        if parts.is_cuda:  # one pass over the w rows (csrc/wire.hip), the same bits as below
+            mine = wire.bf16_sum_ranks(parts)
+        else:
+            acc = parts[0].to(torch.float32)
+            for r in range(1, self.world):  # fp32, rank order: the same sum on whichever rank owns the chunk
+                acc += parts[r].to(torch.float32)
+            mine = acc.to(torch.bfloat16)
         self.gathered = torch.empty_like(self.send)
         self.work = dist.all_gather_into_tensor(self.gathered.view(torch.uint8), mine.view(torch.uint8),
                                                 group=self.group, async_op=True)
@@ -184,7 +193,11 @@ class _Bucket:
     def finish(self) -> None:
         self.work.wait()
         if self.transport == "bf16":
-            self.view.reshape(-1).copy_(self.gathered[:self.view.numel()])
+            flat = self.view.reshape(-1)  # a view: the bucket is a contiguous slice
+            if flat.is_cuda:
+                wire.bf16_unpack(self.gathered, flat)
+            else:
+                flat.copy_(self.gathered[:self.view.numel()])
             self.send = self.recv = self.gathered = None
 
     @property
@@ -202,7 +215,8 @@ class ViewDPExchange:
     """One exchange step per training iteration of view-data-parallel rendering."""
 
     def __init__(self, group: Optional[dist.ProcessGroup] = None, bucket_bytes: int = 64 << 20,
-                 compact_below: float = 0.75, debug: bool = False, transport: str = "fp32"):
+                 compact_below: float = 0.75, debug: bool = False, transport: str = "fp32",
+                 force_collectives: bool = False):
         if bucket_bytes < 4:
             raise ValueError("bucket_bytes must hold at least one fp32 value")
         if not 0.0 <= compact_below <= 1.0:
@@ -214,7 +228,14 @@ class ViewDPExchange:
         self.bucket_bytes = int(bucket_bytes)
         self.compact_below = float(compact_below)
         self.debug = debug
+        # tests and hardware checks: a one-rank group takes the N-rank path (its collectives are real
+        # RCCL calls, so the 1-GPU box exercises every one the 8-GPU bench issues)
+        self.force_collectives = bool(force_collectives)
         self.last = ExchangeStats()
+
+    def _solo(self) -> bool:
+        """One rank and nothing forced: every sum is its input, no collective is issued."""
+        return dist.get_world_size(self.group) == 1 and not self.force_collectives
 
     # ---- visibility -------------------------------------------------------------
     def gather_visibility(self, visible: torch.Tensor):
@@ -222,7 +243,7 @@ class ViewDPExchange:
         if visible.dtype != torch.bool or visible.dim() != 1:
             raise ValueError("visible must be a 1-D bool mask")
         world = dist.get_world_size(self.group)
-        if world == 1:  # one view: nothing to exchange
+        if self._solo():  # one view: nothing to exchange
             return visible.clone(), visible.to(torch.float32).unsqueeze(1)
         bits = pack_mask(visible)
         flat = bits.new_empty((world * bits.numel(),))
@@ -254,7 +275,7 @@ class ViewDPExchange:
                 after(i)
 
     def _all_reduce_buckets(self, flat: torch.Tensor) -> None:
-        if dist.get_world_size(self.group) == 1:  # the sum over one rank is the tensor itself
+        if self._solo():  # the sum over one rank is the tensor itself
             return
         per = max(1, self.bucket_bytes // flat.element_size())
         self._run_buckets([self._bucket(flat[s:s + per]) for s in range(0, flat.numel(), per)])
@@ -291,7 +312,7 @@ class ViewDPExchange:
                 if bool(g.reshape(n, -1)[outside].ne(0).any()):
                     raise RuntimeError("view-DP: a gradient row outside the visibility union is non-zero; "
                                        "the compacted exchange would desynchronise the replicas")
-        if dist.get_world_size(self.group) == 1:  # one rank: the sum is the input, in place already
+        if self._solo():  # one rank: the sum is the input, in place already
             self.last.union_rows = -1  # not counted: no host synchronisation on the one-rank path
             return
         rows = None
@@ -333,7 +354,7 @@ class ViewDPExchange:
     def max_stats(self, stats: List[torch.Tensor]) -> None:
         """In-place MAX over ranks of per-step maxima, all in ONE collective."""
         stats = [s for s in stats if s is not None]
-        if not stats or dist.get_world_size(self.group) == 1:
+        if not stats or self._solo():
             return
         flat = torch.cat([s.reshape(-1).to(torch.float32) for s in stats])
         dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=self.group)
@@ -394,9 +415,9 @@ class ViewDPExchange:
         self.last = ExchangeStats()
         union, count = self.gather_visibility(visible)
         n = arena.n
-        world = dist.get_world_size(self.group)
-        nu = int(union.sum()) if n and world > 1 else 0  # (no host synchronisation on one rank)
-        if world == 1 or n == 0 or nu < self.compact_below * n:
+        solo = self._solo()
+        nu = int(union.sum()) if n and not solo else 0  # (no host synchronisation on one rank)
+        if solo or n == 0 or nu < self.compact_below * n:
             self.sum_gradients(arena, union)
             optimizer.begin_step(union).run()  # counters advance only once the gradients are summed
         else:

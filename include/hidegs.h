@@ -26,6 +26,8 @@
  *   hidegs_masked_adam          <- the per-parameter update of scene/OurAdam.py (_single_tensor_adam :249-337,
  *                                  _single_tensor_adam2 :340-420)
  *   hidegs_masked_adam_multi    <- the loop over parameters of Adam.step(relevant) (scene/OurAdam.py:106-175)
+ *   hidegs_bf16_pack / _sum_ranks / _unpack  <- no reference counterpart: the bf16 wire of the view-DP
+ *                                  exchange (the reference trains on one GPU)
  * INTEGRATION.md shows the Python-side bindings.
  */
 #ifndef HIDEGS_H_INCLUDED
@@ -203,6 +205,19 @@ typedef struct hidegs_adam_tensor {
  * in one launch per 8 tensors.  `tensors` is a host array of `count` descriptors.
  */
 int hidegs_masked_adam_multi(const hidegs_adam_tensor* tensors, int count, void* stream);
+
+/*
+ * bf16 wire format of the view-DP gradient exchange (hidegs_amd/view_dp.py, transport "bf16"), bit for
+ * bit the torch definitions of hidegs_amd/csrc/wire.hip.  bf16 values are uint16_t bit patterns.
+ *   hidegs_bf16_pack:      dst[i] = bf16(src[i]) (round to nearest even, NaN -> 0x7FC0) for i < n,
+ *                          0 for n <= i < n_padded.
+ *   hidegs_bf16_sum_ranks: out[j] = bf16(fp32 sum of parts[r * chunk + j] for r = 0 .. world-1, added in
+ *                          rank order), j < chunk.
+ *   hidegs_bf16_unpack:    dst[i] = float(src[i]) (exact), i < n.
+ */
+int hidegs_bf16_pack(const float* src, uint16_t* dst, long long n, long long n_padded, void* stream);
+int hidegs_bf16_sum_ranks(const uint16_t* parts, int world, long long chunk, uint16_t* out, void* stream);
+int hidegs_bf16_unpack(const uint16_t* src, float* dst, long long n, void* stream);
 
 /*
  * [host] Per-kernel device timing.  While enabled, every kernel this library launches is

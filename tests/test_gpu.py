@@ -95,3 +95,76 @@ def test_exchange_and_step_over_rccl_single_rank_equals_step():
             assert torch.equal(pa[k].detach(), pb[k].detach()), k
     finally:
         dist.destroy_process_group()
+
+
+def _one_rank_nccl():
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    return dist
+
+
+@pytest.mark.parametrize("transport", ["fp32", "bf16"])
+@pytest.mark.parametrize("compact_below", [0.0, 1.0])
+def test_view_dp_collectives_on_rccl_forced_single_rank(transport, compact_below):
+    """Every RCCL call of the N-rank exchange on real hardware: a one-rank group with the N-rank path
+    forced (visibility all-gather, bucketed async all-reduce or bf16 all-to-all + all-gather, compacted
+    or dense, the MAX all-reduce).  Over one rank the sum is the input (bf16 wire: rounded to bf16)."""
+    from hidegs_amd.view_dp import LEAF_WIDTHS, ViewDPExchange
+    dist = _one_rank_nccl()
+    try:
+        n = 100_003
+        g = torch.Generator(device="cuda").manual_seed(11)
+        visible = torch.rand(n, device="cuda", generator=g) < 0.4
+        grads = {k: torch.randn(n, w, device="cuda", generator=g) * visible[:, None] for k, w in LEAF_WIDTHS.items()}
+        ref = {k: (v.to(torch.bfloat16).float() if transport == "bf16" else v.clone()) for k, v in grads.items()}
+        gmax = torch.rand(n, device="cuda", generator=g)
+        gm = gmax.clone()
+        ex = ViewDPExchange(bucket_bytes=1 << 20, compact_below=compact_below, transport=transport,
+                            force_collectives=True)
+        res = ex.exchange(grads, visible, max_stats=[gm])
+        torch.cuda.synchronize()
+        assert ex.last.collectives >= 3 and ex.last.compacted == (compact_below == 1.0)
+        assert torch.equal(res.union, visible)
+        assert torch.equal(res.view_count.squeeze(1), visible.float())
+        assert torch.equal(gm, gmax)
+        for k in grads:
+            assert torch.equal(grads[k], ref[k]), k
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("transport", ["fp32", "bf16"])
+def test_exchange_and_step_on_rccl_forced_single_rank(transport):
+    """The overlapped path on hardware (every bucket's collective issued, then per bucket its wait
+    and that bucket's rows' masked Adam step): equals Adam.step(visible) on the summed gradients."""
+    from hidegs_amd.optim import Adam
+    from hidegs_amd.view_dp import LEAF_WIDTHS, GradArena, ViewDPExchange
+    dist = _one_rank_nccl()
+    try:
+        n = 50_001
+        g = torch.Generator(device="cuda").manual_seed(12)
+        visible = torch.rand(n, device="cuda", generator=g) < 0.8
+        init = {k: torch.randn(n, w, device="cuda", generator=g) for k, w in LEAF_WIDTHS.items()}
+        grads = {k: torch.randn(n, w, device="cuda", generator=g) for k, w in LEAF_WIDTHS.items()}
+        pa = {k: torch.nn.Parameter(v.clone()) for k, v in init.items()}
+        pb = {k: torch.nn.Parameter(v.clone()) for k, v in init.items()}
+        arena = GradArena(n, device="cuda")
+        arena.attach(pb)
+        for k in LEAF_WIDTHS:
+            pa[k].grad = grads[k].to(torch.bfloat16).float() if transport == "bf16" else grads[k].clone()
+            arena[k].copy_(grads[k])
+        Adam(list(pa.values()), lr=0.01, eps=1e-15).step(visible)
+        ex = ViewDPExchange(bucket_bytes=256 << 10, compact_below=0.0, transport=transport, force_collectives=True)
+        res = ex.exchange_and_step(arena, visible, Adam(list(pb.values()), lr=0.01, eps=1e-15), pb)
+        torch.cuda.synchronize()
+        assert ex.last.collectives > len(LEAF_WIDTHS) and torch.equal(res.union, visible)
+        for k in LEAF_WIDTHS:
+            assert torch.equal(pa[k].detach(), pb[k].detach()), k
+    finally:
+        dist.destroy_process_group()
