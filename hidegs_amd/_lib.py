@@ -72,6 +72,8 @@ SIGNATURES = {
     "hidegs_bf16_pack": (I, [P, P, LL, LL, P]),
     "hidegs_bf16_sum_ranks": (I, [P, I, LL, P, P]),
     "hidegs_bf16_unpack": (I, [P, P, LL, P]),
+    "hidegs_mask_pack": (I, [P, LL, P, P]),
+    "hidegs_mask_union_count": (I, [P, I, LL, P, P, P]),
     "hidegs_kernel_timing": (None, [I]),
     "hidegs_kernel_timing_reset": (None, []),
     "hidegs_kernel_time": (I, [C.c_char_p, P, P]),

@@ -1,5 +1,6 @@
-// wire.hip -- the bf16 wire format of the view-DP gradient exchange ("optionally
-// bf16 transport, behind a parity flag"; hidegs_amd/view_dp.py, transport="bf16").
+// wire.hip -- the local steps of the view-DP exchange around its collectives (SURVEY §8(e) E2;
+// hidegs_amd/view_dp.py): the visibility masks' bit packing and union / view count, and the bf16
+// wire format ("optionally bf16 transport, behind a parity flag": transport="bf16").
 //
 // One bucket of fp32 gradients travels as bf16: packed (round to nearest even), split into one
 // chunk per rank and handed to its owner by an all-to-all, summed there in fp32 in rank order and
@@ -113,6 +114,33 @@ __global__ __launch_bounds__(kBlock) void bf16_unpack_kernel(const uint16_t* __r
     }
 }
 
+// Visibility masks (the exchange's first collective): bits[j] = sum_i (mask[8j + i] != 0) << i.
+__global__ __launch_bounds__(kBlock) void mask_pack_kernel(const uint8_t* __restrict__ mask, long long n,
+                                                           uint8_t* __restrict__ bits)
+{
+    const long long j = (long long)blockIdx.x * kBlock + threadIdx.x;
+    const long long i0 = 8 * j;
+    if (i0 >= n) return;
+    uint32_t b = 0;
+    for (int i = 0; i < 8; i++)
+        if (i0 + i < n && mask[i0 + i]) b |= 1u << i;
+    bits[j] = (uint8_t)b;
+}
+
+// After the all-gather of `ranks` packed masks (rows of nbytes): every Gaussian's view count over the
+// ranks and its union bit -- unpack_mask + sum + compare of the torch definition, in one pass.
+__global__ __launch_bounds__(kBlock) void mask_union_count_kernel(const uint8_t* __restrict__ bits, int ranks,
+                                                                  long long nbytes, long long n,
+                                                                  uint8_t* __restrict__ any, float* __restrict__ count)
+{
+    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint32_t c = 0;
+    for (int r = 0; r < ranks; r++) c += (bits[(long long)r * nbytes + (i >> 3)] >> (i & 7)) & 1u;
+    any[i] = c != 0;
+    count[i] = (float)c;
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 unsigned grid_for(long long n)
@@ -160,4 +188,28 @@ extern "C" int hidegs_bf16_unpack(const uint16_t* src, float* dst, long long n, 
     HIDEGS_LAUNCH("bf16_unpack", bf16_unpack_kernel, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), src, dst, n,
                   vec);
     return check_launch("bf16_unpack", as_stream(stream), 0);
+}
+
+extern "C" int hidegs_mask_pack(const unsigned char* mask, long long n, unsigned char* bits, void* stream)
+{
+    using namespace hidegs;
+    if (n < 0 || n > (long long)kBlock * 8 * 0x7fffffffLL) return fail(HIDEGS_E_ARG, "mask_pack: bad size");
+    if (n == 0) return 0;
+    if (!mask || !bits) return fail(HIDEGS_E_ARG, "mask_pack: NULL pointer");
+    const long long nb = (n + 7) / 8;
+    HIDEGS_LAUNCH("mask_pack", mask_pack_kernel, dim3((unsigned)((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                  as_stream(stream), mask, n, bits);
+    return check_launch("mask_pack", as_stream(stream), 0);
+}
+
+extern "C" int hidegs_mask_union_count(const unsigned char* bits, int ranks, long long n, unsigned char* any,
+                                       float* count, void* stream)
+{
+    using namespace hidegs;
+    if (ranks < 1 || n < 0 || n > (long long)kBlock * 0x7fffffffLL) return fail(HIDEGS_E_ARG, "mask_union_count: bad sizes");
+    if (n == 0) return 0;
+    if (!bits || !any || !count) return fail(HIDEGS_E_ARG, "mask_union_count: NULL pointer");
+    HIDEGS_LAUNCH("mask_union_count", mask_union_count_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)),
+                  dim3(kBlock), 0, as_stream(stream), bits, ranks, (n + 7) / 8, n, any, count);
+    return check_launch("mask_union_count", as_stream(stream), 0);
 }

@@ -245,10 +245,13 @@ class ViewDPExchange:
         world = dist.get_world_size(self.group)
         if self._solo():  # one view: nothing to exchange
             return visible.clone(), visible.to(torch.float32).unsqueeze(1)
-        bits = pack_mask(visible)
+        cuda = visible.is_cuda
+        bits = wire.mask_pack(visible.contiguous()) if cuda else pack_mask(visible)
         flat = bits.new_empty((world * bits.numel(),))
         dist.all_gather_into_tensor(flat, bits, group=self.group)
         self.last.collectives += 1
+        if cuda:  # one pass (csrc/wire.hip), the same result as the torch definition below
+            return wire.mask_union_count(flat.view(world, bits.numel()), visible.numel())
         per_rank = unpack_mask(flat.view(world, bits.numel()), visible.numel())
         count = per_rank.sum(0, dtype=torch.int32)
         return count > 0, count.to(torch.float32).unsqueeze(1)

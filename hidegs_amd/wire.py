@@ -63,3 +63,34 @@ def bf16_unpack(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
         rc = _lib.lib().hidegs_bf16_unpack(_lib.ptr(src), _lib.ptr(dst), dst.numel(), _lib.stream_handle(dev))
     _lib.check(rc, "bf16_unpack")
     return dst
+
+
+def mask_pack(mask: torch.Tensor) -> torch.Tensor:
+    """bool (N,) -> uint8 (ceil(N/8),), bit i of byte j = mask[8j + i] (view_dp.pack_mask's bits)."""
+    if mask.dtype != torch.bool or mask.dim() != 1 or not mask.is_contiguous():
+        raise RuntimeError("mask_pack: expected a contiguous 1-D bool mask")
+    bits = torch.empty((mask.numel() + 7) // 8, dtype=torch.uint8, device=mask.device)
+    if mask.numel() == 0:
+        return bits
+    dev = _lib.device_of(mask, bits)
+    with torch.cuda.device(dev):
+        rc = _lib.lib().hidegs_mask_pack(_lib.ptr(mask), mask.numel(), _lib.ptr(bits), _lib.stream_handle(dev))
+    _lib.check(rc, "mask_pack")
+    return bits
+
+
+def mask_union_count(bits: torch.Tensor, n: int):
+    """(R, ceil(n/8)) uint8 packed masks -> (union bool (n,), view count float32 (n, 1)), the
+    definition unpack_mask(bits, n).sum(0) > 0 and its float count, in one pass."""
+    if bits.dtype != torch.uint8 or bits.dim() != 2 or not bits.is_contiguous() or bits.shape[1] != (n + 7) // 8:
+        raise RuntimeError("mask_union_count: expected (ranks, ceil(n/8)) contiguous uint8")
+    union = torch.empty(n, dtype=torch.bool, device=bits.device)
+    count = torch.empty(n, 1, dtype=torch.float32, device=bits.device)
+    if n == 0:
+        return union, count
+    dev = _lib.device_of(bits, union, count)
+    with torch.cuda.device(dev):
+        rc = _lib.lib().hidegs_mask_union_count(_lib.ptr(bits), int(bits.shape[0]), int(n), _lib.ptr(union),
+                                                _lib.ptr(count), _lib.stream_handle(dev))
+    _lib.check(rc, "mask_union_count")
+    return union, count

@@ -26,8 +26,9 @@
  *   hidegs_masked_adam          <- the per-parameter update of scene/OurAdam.py (_single_tensor_adam :249-337,
  *                                  _single_tensor_adam2 :340-420)
  *   hidegs_masked_adam_multi    <- the loop over parameters of Adam.step(relevant) (scene/OurAdam.py:106-175)
- *   hidegs_bf16_pack / _sum_ranks / _unpack  <- no reference counterpart: the bf16 wire of the view-DP
- *                                  exchange (the reference trains on one GPU)
+ *   hidegs_bf16_pack / _sum_ranks / _unpack, hidegs_mask_pack / _union_count
+ *                               <- no reference counterpart: local steps of the view-DP exchange
+ *                                  (the reference trains on one GPU)
  * INTEGRATION.md shows the Python-side bindings.
  */
 #ifndef HIDEGS_H_INCLUDED
@@ -218,6 +219,17 @@ int hidegs_masked_adam_multi(const hidegs_adam_tensor* tensors, int count, void*
 int hidegs_bf16_pack(const float* src, uint16_t* dst, long long n, long long n_padded, void* stream);
 int hidegs_bf16_sum_ranks(const uint16_t* parts, int world, long long chunk, uint16_t* out, void* stream);
 int hidegs_bf16_unpack(const uint16_t* src, float* dst, long long n, void* stream);
+
+/*
+ * Visibility masks of the view-DP exchange (hidegs_amd/view_dp.py gather_visibility), bit for bit its
+ * torch definitions pack_mask / unpack_mask:
+ *   hidegs_mask_pack:        bits[j] = sum over i < 8 of (mask[8j + i] != 0) << i, ceil(n / 8) bytes.
+ *   hidegs_mask_union_count: bits holds `ranks` packed masks of ceil(n / 8) bytes each; for i < n,
+ *                            count[i] = number of ranks with bit i set (float), any[i] = count[i] > 0.
+ */
+int hidegs_mask_pack(const unsigned char* mask, long long n, unsigned char* bits, void* stream);
+int hidegs_mask_union_count(const unsigned char* bits, int ranks, long long n, unsigned char* any, float* count,
+                            void* stream);
 
 /*
  * [host] Per-kernel device timing.  While enabled, every kernel this library launches is

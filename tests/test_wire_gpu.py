@@ -84,3 +84,19 @@ def test_wire_rejects_wrong_dtypes_and_sizes():
         wire.bf16_pack(x, torch.empty(16, dtype=torch.float16, device="cuda"))
     with pytest.raises(RuntimeError):
         wire.bf16_unpack(torch.empty(4, dtype=torch.bfloat16, device="cuda"), x)
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 1000, 2_000_003])
+@pytest.mark.parametrize("ranks", [1, 3, 8])
+def test_mask_pack_and_union_count_match_the_definitions(n, ranks):
+    from hidegs_amd.view_dp import pack_mask, unpack_mask
+    g = torch.Generator(device="cuda").manual_seed(n + ranks)
+    masks = [torch.rand(n, device="cuda", generator=g) < p for p in torch.linspace(0.05, 0.9, ranks).tolist()]
+    packed = [wire.mask_pack(m) for m in masks]
+    for m, b in zip(masks, packed):
+        assert torch.equal(b, pack_mask(m))
+    flat = torch.stack(packed)
+    union, count = wire.mask_union_count(flat, n)
+    ref = unpack_mask(flat, n).sum(0, dtype=torch.int32)
+    assert torch.equal(union, ref > 0)
+    assert torch.equal(count, ref.to(torch.float32).unsqueeze(1))
