@@ -8,7 +8,8 @@ import torch  # noqa: E402
 from hidegs_amd import primitives, synthetic  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-wl = synthetic.binning_workload(2_000_000, device="cuda")
+cam = synthetic.d2_camera(1920, 1080)
+wl = synthetic.d2_binning_workload(synthetic.d2_scene(2_000_000, cam, seed=0), cam, device="cuda")  # the bench's view
 end = 32 + primitives.higher_msb(wl.num_tiles)
 for _ in range(reps):
     primitives.sort_tile_pairs(wl.keys, wl.values, wl.num_tiles)
