@@ -51,7 +51,10 @@ constexpr int kWaves = kBlock / kWave;  // 4 waves = 4 leaves per workgroup
 constexpr int kLeaf = 64;               // points per leaf
 constexpr int kFan = 64;                // leaves per super-box
 constexpr int kSub = 4;                 // sub-boxes per leaf (16 points each): the fine filter
-constexpr int kMortonBits = 16;         // per axis
+#ifndef HIDEGS_KNN_MORTON_BITS
+#define HIDEGS_KNN_MORTON_BITS 16
+#endif
+constexpr int kMortonBits = HIDEGS_KNN_MORTON_BITS;  // per axis (the sort runs over 3x these bits)
 constexpr int kBoundBlocks = 1024;
 constexpr float kHardFactor = 8.0f;     // 3rd-best above 8x the wave mean -> phase 2
 
