@@ -268,7 +268,7 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
     # key 8 + value 4; a histogram pass reads the 8-byte keys; the scan reads and writes u32)
     alg = {"scan_reduce": 4 * N, "scan_small": 0, "scan_downsweep": 8 * N,
            "radix_hist_u64": 8 * K, "radix_digit_scan": 0, "radix_scatter_u64": 24 * K,
-           "segment_sort": 24 * K, "big_segments": 0}
+           "segment_sort": 24 * K, "big_segments": 0, "piece_sort": 0}
 
     def kernel_table(fn, nsteps):
         with _lib.kernel_timer() as kt:

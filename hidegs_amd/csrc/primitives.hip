@@ -968,12 +968,19 @@ constexpr int kQueueMin = HIDEGS_QUEUE_MIN;
 #define HIDEGS_WIDE_CAP 12288  // segments up to this many pairs: one WIDE job (LDS sort by one worker)
 #endif
 constexpr int kWideCap = HIDEGS_WIDE_CAP;
+#ifndef HIDEGS_PIECE_WAVES
+#define HIDEGS_PIECE_WAVES 5  // waves per SIMD piece_sort_kernel's register budget is set for (6: 10 VGPRs spilled)
+#endif
+#ifndef HIDEGS_DEFER_PIECES
+#define HIDEGS_DEFER_PIECES 1  // 0: the queue's pieces run as its own SMALL jobs (one workgroup per CU)
+#endif
+constexpr bool kDeferPieces = HIDEGS_DEFER_PIECES != 0;
 #ifndef HIDEGS_WIDE_SCOUTS
 #define HIDEGS_WIDE_SCOUTS 0  // 1: scouts hand hot tiles of <= kWideCap pairs to the queue as WIDE jobs (slower: DESIGN.md)
 #endif
 constexpr uint32_t kMaxPolls = 1u << 22;
 enum : uint32_t { J_EXIT = 0, J_SMALL, J_COPY, J_REDUCE, J_HIST, J_SCATTER, J_GLOBAL, J_WIDE };
-enum : int { Q_HEAD, Q_RESERVE, Q_DONE, Q_NREC, Q_POOL, Q_ERROR, Q_COUNTERS = 8 };
+enum : int { Q_HEAD, Q_RESERVE, Q_DONE, Q_NREC, Q_POOL, Q_ERROR, Q_NPIECE, Q_COUNTERS = 8 };
 constexpr int kCtlStride = 32;  // one 128-byte line per counter: polls of one do not queue behind another's atomics
 constexpr int Q_WORDS = Q_COUNTERS * kCtlStride;
 static_assert(Q_WORDS <= kBlock, "identify_ranges_kernel zeroes the counters with one workgroup");
@@ -997,6 +1004,8 @@ struct BigQueue {
     uint32_t rec_cap, job_cap, pool_cap;
     uint64_t* alt_k;  // the sort's alternate buffers (the global form of a mildly hot tile)
     uint32_t* alt_v;
+    uint2* piece;     // deferred pieces (begin, m | src << 31) for piece_sort_kernel
+    uint32_t piece_cap;
 };
 
 #ifdef HIDEGS_QUEUE_TRACE  // experiments only: per-job timestamps (tools/queue_trace.py)
@@ -1052,7 +1061,7 @@ constexpr int kMaxRuns = kRadix + 1;
 struct EmitShared {
     uint4 run[kMaxRuns];  // (type | src << 8, a, b, count)
     uint32_t off[kMaxRuns + 1];
-    uint32_t nruns, base;
+    uint32_t nruns, base, pbase;
 };
 
 __device__ __forceinline__ void runs_begin(EmitShared& e)
@@ -1349,12 +1358,34 @@ __device__ __forceinline__ void cut_pieces(const BigQueue& q, EmitShared& e, Big
         }
         const uint32_t next = t + 1 < kRadix ? nx[t + 1] : m;
         uint4 run = make_uint4(0u, 0u, 0u, 0u);
+        bool piece = false;
         if (boundary) {
             if (n_d > (uint32_t)kSegCap)
                 run = n_d <= (uint32_t)kWideCap ? make_uint4(J_WIDE | (dst << 8), begin + s_d, n_d, 1u)
                                                 : record_run(q, begin + s_d, n_d, dst, true, lo_d, hi_d);
-            else if (next - s_d > 1u || dst)
-                run = make_uint4(J_SMALL | (dst << 8), begin + s_d, next - s_d, 1u);
+            else if (next - s_d > 1u || dst) {
+                if (kDeferPieces)
+                    piece = true;
+                else
+                    run = make_uint4(J_SMALL | (dst << 8), begin + s_d, next - s_d, 1u);
+            }
+        }
+        if (kDeferPieces) {  // pieces go to piece_sort_kernel's list (a SMALL job only if it is full)
+            uint32_t npc;
+            const uint32_t pi = block_exclusive_scan(piece ? 1u : 0u, sh.wave, &npc);
+            if (npc) {  // workgroup-uniform
+                if (t == 0)
+                    e.pbase = __hip_atomic_fetch_add(&q.ctl[kCtlStride * Q_NPIECE], npc, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                __syncthreads();
+                if (piece) {
+                    const uint32_t k = e.pbase + pi;
+                    if (k < q.piece_cap)
+                        q.piece[k] = make_uint2(begin + s_d, (next - s_d) | (dst << 31));
+                    else
+                        run = make_uint4(J_SMALL | (dst << 8), begin + s_d, next - s_d, 1u);
+                }
+            }
         }
         uint32_t nruns, total;
         const uint32_t ri = block_exclusive_scan(run.w ? 1u : 0u, sh.wave, &nruns);
@@ -2331,6 +2362,29 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
     }
 }
 
+// The queue's pieces (<= kSegCap pairs each, cut from partitioned hot tiles), sorted after the queue
+// has drained, at segment_sort_kernel's occupancy instead of one queue worker per CU: 7888 pieces of
+// a one-tile view took the queue ~250 us as SMALL jobs.  With no hot tile the list is empty and
+// every workgroup reads one counter and exits.
+constexpr int kPieceBlocks = 256 * HIDEGS_PIECE_WAVES;  // one workgroup per resident slot
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_PIECE_WAVES))) void piece_sort_kernel(
+    uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint64_t* __restrict__ alt_k,
+    const uint32_t* __restrict__ alt_v, const BigQueue q)
+{
+    __shared__ __attribute__((aligned(16))) SegLds lds;
+    __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock], s_max[kWavesPerBlock];
+    const uint32_t np = min(q.ctl[kCtlStride * Q_NPIECE], q.piece_cap);
+    for (uint32_t p = blockIdx.x; p < np; p += gridDim.x) {
+        const uint2 e = q.piece[p];
+        const uint32_t m = e.y & 0x7fffffffu;
+        if (e.y >> 31)
+            sort_segment<false>(alt_k, alt_v, keys, vals, e.x, m, lds, s_and, s_or, s_max);
+        else
+            sort_segment<true>(keys, vals, nullptr, nullptr, e.x, m, lds, s_and, s_or, s_max);
+        __syncthreads();  // the LDS is reused by the next piece
+    }
+}
+
 // ============================== tile ranges ====================================
 
 // Tile ids >= num_tiles violate the caller contract; their entries are skipped rather
@@ -2412,6 +2466,7 @@ BigQueue queue_caps(long long n)
     q.job_cap = (uint32_t)(n / 24 + 1024);
 #endif
     q.pool_cap = (uint32_t)(n / 2 + 16 * kRadix);
+    q.piece_cap = (uint32_t)(n / 512 + 1024);  // <= 2 pieces per kSegRun pairs; beyond: SMALL jobs
     return q;
 }
 
@@ -2426,7 +2481,7 @@ size_t sort_scratch(long long n)
         b += align_up(sizeof(uint32_t) * (((size_t)1 << kMaxSegmentBits) + 1)) + align_up(kRadix * sizeof(uint32_t)) +
              align_up(Q_WORDS * sizeof(uint32_t)) +
              align_up((size_t)q.rec_cap * sizeof(BigSeg)) + align_up((size_t)q.job_cap * sizeof(uint4)) +
-             align_up((size_t)q.pool_cap * sizeof(uint32_t));
+             align_up((size_t)q.pool_cap * sizeof(uint32_t)) + align_up((size_t)q.piece_cap * sizeof(uint2));
     }
     return b;
 }
@@ -2495,6 +2550,7 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         q.pool = c.take<uint32_t>(q.pool_cap);
         q.alt_k = reinterpret_cast<uint64_t*>(alt_k);
         q.alt_v = alt_v;
+        q.piece = c.take<uint2>(q.piece_cap);
     }
 
     const K* src_k = keys_in;
@@ -2541,6 +2597,9 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
                       vals_out, seg_starts, ranges_out, nseg, q);
         HIDEGS_LAUNCH("big_segments", big_segment_kernel, dim3(kQueueBlocks), dim3(kBlock), 0, stream, ko, vals_out,
                       reinterpret_cast<uint64_t*>(alt_k), alt_v, q);
+        if (kDeferPieces)
+            HIDEGS_LAUNCH("piece_sort", piece_sort_kernel, dim3(kPieceBlocks), dim3(kBlock), 0, stream, ko, vals_out,
+                          reinterpret_cast<const uint64_t*>(alt_k), alt_v, q);
         if (debug_enabled()) {  // debug mode: the queue's own error word, after the grid has drained
             if (int rc = check_launch(what, stream, 1)) return rc;
             uint32_t err = 0;
