@@ -918,8 +918,9 @@ static_assert(sizeof(BucketShared) >= kSegRun * (sizeof(uint64_t) + sizeof(uint3
 //                                                             destinations
 //   SCATTER  the chunk's pairs, ranked stably, to the other buffer (keys <-> alt)
 // and the last SCATTER cuts the result into pieces by digit: runs of small digits merged up to
-// kSegCap pairs become SMALL jobs (the bucket form of segment_sort_kernel, alt -> keys or in place),
-// a digit of more than kSegCap pairs a new record one digit lower.  Each level fixes the top <= 8
+// kSegCap pairs become pieces (the bucket form of segment_sort_kernel, alt -> keys or in place,
+// sorted by piece_sort_kernel after the queue; SMALL jobs only if its list is full), a digit of
+// kSegCap..kWideCap pairs one WIDE job, a bigger digit a new record one digit lower.  Each level fixes the top <= 8
 // varying bits, so the chain ends within 4 levels; pieces left in alt are copied back (COPY jobs).
 // Every piece keeps its pairs in input order between equal digits, so the whole is the stable sort.
 //
