@@ -38,6 +38,7 @@ VARIANTS = {
     "qcap": (["-DHIDEGS_JOB_CAP=64"], ["primitives.hip"]),  # partition-queue overflow -> error word
     "gform": (["-DHIDEGS_QUEUE_MIN=8192"], ["primitives.hip"]),  # tiles of 2049..8192 pairs: one-workgroup global form
     "wscout": (["-DHIDEGS_WIDE_SCOUTS=1"], ["primitives.hip"]),  # hot tiles <= 12288 pairs as WIDE jobs (in place)
+    "pcap": (["-DHIDEGS_PIECE_CAP=16"], ["primitives.hip"]),  # piece list full after 16: the rest as SMALL jobs
 }
 
 

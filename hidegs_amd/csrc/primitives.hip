@@ -2467,7 +2467,11 @@ BigQueue queue_caps(long long n)
     q.job_cap = (uint32_t)(n / 24 + 1024);
 #endif
     q.pool_cap = (uint32_t)(n / 2 + 16 * kRadix);
+#ifdef HIDEGS_PIECE_CAP  // tests only: a tiny piece list sends the pieces beyond it to SMALL jobs
+    q.piece_cap = (uint32_t)HIDEGS_PIECE_CAP;
+#else
     q.piece_cap = (uint32_t)(n / 512 + 1024);  // <= 2 pieces per kSegRun pairs; beyond: SMALL jobs
+#endif
     return q;
 }
 

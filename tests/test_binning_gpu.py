@@ -626,3 +626,22 @@ def test_queue_hand_offs_under_concurrent_load(case):
         torch.cuda.synchronize()
         assert torch.equal(ko, ek) and torch.equal(vo, ev), f"repetition {it}"
         assert primitives.queue_error() == 0
+
+
+def test_pieces_beyond_a_full_piece_list_variant():
+    """The queue's pieces go to piece_sort_kernel's list; a build whose list holds 16 (build.VARIANTS['pcap'])
+    runs every later piece as a SMALL queue job -- the same result, bit for bit, on a D2 view with hot
+    tiles of every size class (opened locally, records, WIDE digits)."""
+    from hidegs_amd import _lib, build, synthetic
+    var = _lib.load_library(build.variant_path("pcap"))
+    cam = synthetic.d2_camera(1920, 1080)
+    wl = synthetic.d2_binning_workload(synthetic.d2_scene(1_000_000, cam, seed=77, cluster=(0.3, 0.05)), cam)
+    keys = wl.keys.numpy().view(np.uint64)
+    vals = wl.values.numpy().view(np.uint32)
+    T = wl.num_tiles
+    ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
+    rc, ko, vo, r = _variant_sort_tile_pairs(var, wl.keys.cuda(), wl.values.cuda(), T)
+    assert rc == 0
+    assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert np.array_equal(ko.cpu().numpy().view(np.uint64), ek)
+    assert np.array_equal(r.cpu().numpy().view(np.uint32), binning.tile_ranges(ek, T))
