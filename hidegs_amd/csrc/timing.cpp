@@ -45,9 +45,16 @@ void resolve_locked()
 
 bool kernel_timing_enabled() { return g_enabled.load(std::memory_order_relaxed); }
 
+// Timing-only events: no system-scope fence when they are recorded.  A default event writes the
+// L2 back and invalidates it at the record, which the measured interval then includes (the
+// radix_scatter launch read 46.7 us this way against rocprofv3's 43.6 us); the host still waits
+// for the stop event in hipEventSynchronize.
+constexpr unsigned kTimerEventFlags = hipEventDisableSystemFence;
+
 LaunchTimer::LaunchTimer(const char* n, hipStream_t s) : name(n), stream(s)
 {
-    if (hipEventCreate(&start) != hipSuccess || hipEventCreate(&stop) != hipSuccess) {
+    if (hipEventCreateWithFlags(&start, kTimerEventFlags) != hipSuccess ||
+        hipEventCreateWithFlags(&stop, kTimerEventFlags) != hipSuccess) {
         start = stop = nullptr;
         return;
     }
