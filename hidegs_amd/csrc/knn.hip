@@ -345,6 +345,10 @@ constexpr int kBailout = HIDEGS_KNN_BAILOUT;  // candidate leaves after which a 
 #ifndef HIDEGS_KNN_SEED_NEIGHBORS
 #define HIDEGS_KNN_SEED_NEIGHBORS 1  // 0: seed from the own leaf only (A/B builds)
 #endif
+#ifndef HIDEGS_KNN_SEED_FILTER
+#define HIDEGS_KNN_SEED_FILTER 1  // neighbour seeds through the group point filter (0: all 128 evaluated):
+                                  // knn_leaf frustum 836/831 -> 815/814 us, uniform 784/787 -> 773/765 (2M)
+#endif
 #ifndef HIDEGS_KNN_SCALAR_SUBS
 #define HIDEGS_KNN_SCALAR_SUBS 1  // sub-boxes by scalar loads (0: vector loads + readlanes): 893 -> 840 us frustum,
                                   // 848 -> 787 uniform, 448 -> 492 plane (2M points)
@@ -425,12 +429,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_K
         const int ln = L - 1, rn = L + 1;
         const float4 pl = ln >= 0 ? sp[ln * kLeaf + lane] : p;
         const float4 pr = rn < nleaves ? sp[min(rn * kLeaf + lane, P - 1)] : p;
+#if HIDEGS_KNN_SEED_FILTER
+        // A neighbour point is evaluated only if it lies within some query group's bound of that
+        // group's box (boxes and bounds over every valid lane, so each lane's three best come out
+        // exactly as from evaluating all 64: a skipped point is at least its bound from every query)
+        float4 slo[kGroups], shi[kGroups];
+        float sub[kGroups];
+        group_boxes(p, valid, slo, shi);
+        group_bounds(b2, valid, sub);
+        auto seed_filtered = [&](const float4 pt, const int nc) {
+            bool usable = false;
+#pragma unroll
+            for (int g = 0; g < kGroups; g++) usable |= box_point_lb(Box{slo[g], shi[g]}, pt) <= sub[g];
+            uint64_t pm = __ballot(usable && lane < nc);
+            while (pm) {
+                const int k = __builtin_ctzll(pm);
+                pm &= pm - 1;
+                kbest(sqdist(p, make_float4(uniform_lane(pt.x, k), uniform_lane(pt.y, k), uniform_lane(pt.z, k), 0.f)),
+                      b0, b1, b2);
+            }
+        };
+        if (ln >= 0) seed_filtered(pl, kLeaf);
+        if (rn < nleaves) {
+            seed_filtered(pr, min(kLeaf, P - rn * kLeaf));
+        }
+#else
         if (ln >= 0)
             for (int k0 = 0; k0 < kLeaf; k0 += kChunk) eval_lanes(pl, k0, kLeaf, -1, p, b0, b1, b2);
         if (rn < nleaves) {
             const int nr = min(kLeaf, P - rn * kLeaf);
             for (int k0 = 0; k0 < nr; k0 += kChunk) eval_lanes(pr, k0, nr, -1, p, b0, b1, b2);
         }
+#endif
 #endif
     }
 
