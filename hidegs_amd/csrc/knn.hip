@@ -250,18 +250,7 @@ __global__ __launch_bounds__(kBlock) void morton_kernel(const float* __restrict_
     vals[i] = (uint32_t)i;
 }
 
-// ---- 3. gather into sorted order ----------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void gather_kernel(const float* __restrict__ pts, const uint32_t* __restrict__ order,
-                                                        int P, float4* __restrict__ sp)
-{
-    const int j = blockIdx.x * kBlock + threadIdx.x;
-    if (j >= P) return;
-    const uint32_t i = order[j];
-    if (i >= (uint32_t)P) return;  // a permutation of [0, P) by construction
-    sp[j] = make_float4(pts[3ll * i], pts[3ll * i + 1], pts[3ll * i + 2], __uint_as_float(i));
-}
-
-// ---- 4. leaf and super boxes ----------------------------------------------------------------
+// ---- 3./4. gather into sorted order; leaf and super boxes ---------------------------------------
 __device__ __forceinline__ Box wave_box(float4 p, bool valid)
 {
     Box b;
@@ -270,16 +259,11 @@ __device__ __forceinline__ Box wave_box(float4 p, bool valid)
     return b;
 }
 
-// Leaf boxes and, per leaf, kSub sub-boxes of kLeaf / kSub consecutive points (the fine filter).
-__global__ __launch_bounds__(kBlock) void leaf_box_kernel(const float4* __restrict__ sp, int P, int nleaves,
-                                                          Box* __restrict__ leaves, Box* __restrict__ subs)
+// Leaf L's box and its kSub sub-boxes of kLeaf / kSub consecutive points (the fine filter), from the
+// wave holding the leaf's points (lane = point in leaf).
+__device__ __forceinline__ void store_leaf_boxes(const float4 p, const bool valid, const int L, const int lane,
+                                                 Box* __restrict__ leaves, Box* __restrict__ subs)
 {
-    const int L = blockIdx.x * kWaves + threadIdx.x / kWave;
-    if (L >= nleaves) return;
-    const int lane = lane_id();
-    const int i = L * kLeaf + lane;
-    const bool valid = i < P;
-    const float4 p = valid ? sp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     float v[6] = {valid ? p.x : FLT_MAX,  valid ? p.y : FLT_MAX,  valid ? p.z : FLT_MAX,
                   valid ? p.x : -FLT_MAX, valid ? p.y : -FLT_MAX, valid ? p.z : -FLT_MAX};
     // reduce inside groups of kLeaf / kSub lanes, store the sub-box, then finish across groups
@@ -300,6 +284,47 @@ __global__ __launch_bounds__(kBlock) void leaf_box_kernel(const float4* __restri
             v[a] = a < 3 ? fminf(v[a], o) : fmaxf(v[a], o);
         }
     if (lane == 0) leaves[L] = Box{make_float4(v[0], v[1], v[2], 0.f), make_float4(v[3], v[4], v[5], 0.f)};
+}
+
+#ifndef HIDEGS_KNN_FUSED_BOX
+#define HIDEGS_KNN_FUSED_BOX 1  // the gather also writes the leaf and sub-boxes (0: a leaf_box launch rereads the
+                                // sorted array): distCUDA2 frustum 1143/1146 -> 1138/1125 us, uniform 1066/1063 -> 1056/1026
+#endif
+// Sorted point j = original point order[j] as {x, y, z, bits(original index)}.  With Boxes, wave w of
+// block b holds leaf 4b + w (kLeaf == kWave) and also writes its boxes: the reductions of
+// leaf_box_kernel on the same values, so the same bits, without reading the sorted array again.
+template <bool Boxes>
+__global__ __launch_bounds__(kBlock) void gather_kernel(const float* __restrict__ pts, const uint32_t* __restrict__ order,
+                                                        int P, float4* __restrict__ sp, int nleaves,
+                                                        Box* __restrict__ leaves, Box* __restrict__ subs)
+{
+    static_assert(kLeaf == kWave, "one wave per leaf");
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool valid = false;
+    if (j < P) {
+        const uint32_t i = order[j];
+        if (i < (uint32_t)P) {  // a permutation of [0, P) by construction
+            p = make_float4(pts[3ll * i], pts[3ll * i + 1], pts[3ll * i + 2], __uint_as_float(i));
+            sp[j] = p;
+            valid = true;
+        }
+    }
+    if (!Boxes) return;
+    const int L = j / kLeaf;  // wave-uniform
+    if (L >= nleaves) return;  // whole wave
+    store_leaf_boxes(p, valid, L, lane_id(), leaves, subs);
+}
+
+__global__ __launch_bounds__(kBlock) void leaf_box_kernel(const float4* __restrict__ sp, int P, int nleaves,
+                                                          Box* __restrict__ leaves, Box* __restrict__ subs)
+{
+    const int L = blockIdx.x * kWaves + threadIdx.x / kWave;
+    if (L >= nleaves) return;
+    const int lane = lane_id();
+    const int i = L * kLeaf + lane;
+    const bool valid = i < P;
+    store_leaf_boxes(valid ? sp[i] : make_float4(0.f, 0.f, 0.f, 0.f), valid, L, lane, leaves, subs);
 }
 
 __global__ __launch_bounds__(kBlock) void super_box_kernel(const Box* __restrict__ leaves, int nleaves, int nsuper,
@@ -829,9 +854,15 @@ int dist_cuda2(hidegs_alloc_fn alloc, void* user, int P, const float* points, fl
     int rc = sort_pairs_u64(l.sort_tmp, l.sort_bytes, l.keys, l.keys_sorted, l.vals, l.vals_sorted, P, 0,
                             3 * kMortonBits, stream);
     if (rc) return rc;
-    HIDEGS_LAUNCH("gather", gather_kernel, dim3(nb), dim3(kBlock), 0, stream, points, l.vals_sorted, P, l.sp);
-    HIDEGS_LAUNCH("leaf_box", leaf_box_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P, nleaves,
-                       l.leaves, l.subs);
+    if (HIDEGS_KNN_FUSED_BOX) {
+        HIDEGS_LAUNCH("gather", gather_kernel<true>, dim3(nb), dim3(kBlock), 0, stream, points, l.vals_sorted, P, l.sp,
+                      nleaves, l.leaves, l.subs);
+    } else {
+        HIDEGS_LAUNCH("gather", gather_kernel<false>, dim3(nb), dim3(kBlock), 0, stream, points, l.vals_sorted, P, l.sp,
+                      nleaves, l.leaves, l.subs);
+        HIDEGS_LAUNCH("leaf_box", leaf_box_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P,
+                      nleaves, l.leaves, l.subs);
+    }
     HIDEGS_LAUNCH("super_box", super_box_kernel, dim3(ceil_div(nsuper, kWaves)), dim3(kBlock), 0, stream, l.leaves, nleaves,
                        nsuper, l.supers);
     HIDEGS_LAUNCH("knn_leaf", knn_leaf_kernel, dim3(ceil_div(nleaves, kWaves)), dim3(kBlock), 0, stream, l.sp, P, nleaves,
