@@ -55,6 +55,11 @@ constexpr int kSub = 4;                 // sub-boxes per leaf (16 points each): 
 #define HIDEGS_KNN_MORTON_BITS 16
 #endif
 constexpr int kMortonBits = HIDEGS_KNN_MORTON_BITS;  // per axis (the sort runs over 3x these bits)
+#ifndef HIDEGS_KNN_SORT_BEGIN
+#define HIDEGS_KNN_SORT_BEGIN 0  // low Morton bits left out of the sort (the order changes speed only)
+#endif
+constexpr int kSortBegin = HIDEGS_KNN_SORT_BEGIN;
+static_assert(kSortBegin >= 0 && kSortBegin < 3 * kMortonBits, "HIDEGS_KNN_SORT_BEGIN: inside the code");
 constexpr int kBoundBlocks = 1024;
 constexpr float kHardFactor = 8.0f;     // 3rd-best above 8x the wave mean -> phase 2
 
@@ -851,7 +856,7 @@ int dist_cuda2(hidegs_alloc_fn alloc, void* user, int P, const float* points, fl
     HIDEGS_LAUNCH("bounds", bounds_kernel, dim3(nbound), dim3(kBlock), 0, stream, points, P, l.partials);
     HIDEGS_LAUNCH("bounds_finalize", bounds_finalize_kernel, dim3(1), dim3(kBlock), 0, stream, l.partials, nbound, l.params);
     HIDEGS_LAUNCH("morton", morton_kernel, dim3(nb), dim3(kBlock), 0, stream, points, P, l.params, l.keys, l.vals);
-    int rc = sort_pairs_u64(l.sort_tmp, l.sort_bytes, l.keys, l.keys_sorted, l.vals, l.vals_sorted, P, 0,
+    int rc = sort_pairs_u64(l.sort_tmp, l.sort_bytes, l.keys, l.keys_sorted, l.vals, l.vals_sorted, P, kSortBegin,
                             3 * kMortonBits, stream);
     if (rc) return rc;
     if (HIDEGS_KNN_FUSED_BOX) {
