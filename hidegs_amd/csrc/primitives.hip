@@ -313,14 +313,14 @@ constexpr int kSItems = kTile / kSBlock;  // pairs per thread
 static_assert(kSBlock >= kRadix, "one thread per digit in the digit scans");
 
 // radix_scatter_kernel<K, true>'s segment starts (see there); every thread of the workgroup calls it.
-template <typename K, int R>
+template <typename K, int R, int D = kRadix>  // D: digit capacity (> mask, and 1 << b0 <= D)
 __device__ __forceinline__ void segment_starts(const K (&k)[R], const bool (&ok)[R], const int shift, const uint32_t mask,
                                             const long long n, const int tile, const int ntiles,
                                             const long long base, const uint32_t digit_base,
                                             const uint32_t p0, const int b0, uint32_t* starts)
 {
-    __shared__ uint32_t s_bhist[kRadix];
-    __shared__ uint32_t s_blist[kRadix];
+    __shared__ uint32_t s_bhist[D];
+    __shared__ uint32_t s_blist[D];
     __shared__ uint32_t s_nb;
     const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
     if (t == 0) {
@@ -340,7 +340,7 @@ __device__ __forceinline__ void segment_starts(const K (&k)[R], const bool (&ok)
     const uint32_t nb = s_nb;  // workgroup-uniform; 0 for most tiles
     for (uint32_t b = 0; b < nb; b++) {
         const uint32_t e = s_blist[b], L = e & 0xffu, r = e >> 8;  // the tile's pairs [0, r) precede L
-        if (t < kRadix) s_bhist[t] = 0u;
+        if (t < D) s_bhist[t] = 0u;
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < R; q++) {
@@ -361,8 +361,18 @@ __device__ __forceinline__ void segment_starts(const K (&k)[R], const bool (&ok)
 // exclusive scan of pass 0's digit totals, totals0), for the tile that holds base0[L].  b0 == 0
 // (one pass, the digit is the whole segment id): tile 0 writes starts[d] = base of digit d.
 // starts[(mask + 1) << b0] = n closes the last segment.
-template <typename K, bool Starts = false>
-__global__ __launch_bounds__(kSBlock) void radix_scatter_kernel(const K* __restrict__ keys_in,
+// D = digit capacity: kRadix, or kNarrowRadix for passes of <= 7 bits, whose smaller LDS arrays
+// (39 KB instead of 45 KB) let a fourth workgroup onto each CU: the 1080p binning sort (8.6M pairs,
+// 6 + 7 bits) 189 -> 183 us.  Only up to kNarrowMaxN pairs: the 4K frame's 42.9M pairs (7 + 8 bits)
+// went 880 -> 894 us with its 7-bit pass narrow -- a fourth workgroup's open digit runs cost more
+// once a pass's output no longer stays in the 256 MB MALL (profiles/r04_narrow_scatter.md).
+#ifndef HIDEGS_SCATTER_NARROW
+#define HIDEGS_SCATTER_NARROW 1
+#endif
+constexpr int kNarrowRadix = 128;
+constexpr long long kNarrowMaxN = 12ll << 20;
+template <typename K, bool Starts = false, int D = kRadix>
+__global__ __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(D == kRadix ? 1 : 8))) void radix_scatter_kernel(const K* __restrict__ keys_in,
                                                                 const uint32_t* __restrict__ vals_in,
                                                                 K* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
                                                                 long long n, int shift, uint32_t mask, int ntiles,
@@ -372,17 +382,17 @@ __global__ __launch_bounds__(kSBlock) void radix_scatter_kernel(const K* __restr
                                                                 uint32_t* __restrict__ starts)
 {
     __shared__ __attribute__((aligned(16))) K s_stage[kTile];  // keys by tile-local rank, then values
-    __shared__ uint32_t s_cnt[kSWaves][kRadix];         // per-wave running counters
-    __shared__ uint32_t s_start[kRadix];                // tile-local start of each digit run
-    __shared__ uint32_t s_off[kRadix];                  // global position of tile-local position 0 of digit d
+    __shared__ uint32_t s_cnt[kSWaves][D];              // per-wave running counters
+    __shared__ uint32_t s_start[D];                     // tile-local start of each digit run
+    __shared__ uint32_t s_off[D];                       // global position of tile-local position 0 of digit d
     __shared__ uint32_t s_wave[kSWaves];
     uint32_t* s_vals = reinterpret_cast<uint32_t*>(s_stage);
 
     const int t = threadIdx.x;
     const int lane = lane_id();
     const int wave = t / kWave;
-    const bool digit_thread = t < kRadix;  // thread d owns digit d in the digit scans
-    for (int i = t; i < kSWaves * kRadix; i += kSBlock) (&s_cnt[0][0])[i] = 0;
+    const bool digit_thread = t < D;  // thread d owns digit d in the digit scans
+    for (int i = t; i < kSWaves * D; i += kSBlock) (&s_cnt[0][0])[i] = 0;
     const int tile = HIDEGS_XCD_TILES ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const long long base = (long long)tile * kTile;
     const long long seg = base + (long long)wave * (kSItems * kWave);  // this wave's items
@@ -407,7 +417,7 @@ __global__ __launch_bounds__(kSBlock) void radix_scatter_kernel(const K* __restr
     uint32_t dummy;
     const uint32_t digit_base = block_exclusive_scan<kSWaves>(digit_total, s_wave, &dummy) + digit_prefix;
     // (at the end of the kernel instead, with the keys kept live: 73 VGPRs against 61, same time)
-    if (Starts) segment_starts(k, ok, shift, mask, n, tile, ntiles, base, digit_base, low_base, b0, starts);
+    if (Starts) segment_starts<K, kSItems, D>(k, ok, shift, mask, n, tile, ntiles, base, digit_base, low_base, b0, starts);
     uint32_t rank[kSItems];
     wave_rank<K, kSItems>(k, ok, shift, mask, s_cnt[wave], rank, mask);
     __syncthreads();
@@ -2584,14 +2594,26 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         HIDEGS_LAUNCH("radix_digit_scan", radix_digit_scan_kernel, dim3(mask + 1), dim3(kBlock), 0, stream, counts,
                       nt, totals, low ? totals_pass[0] : nullptr, low ? 1 << pass_bits[0] : 0, low_base);
         if (p < 2) pass_bits[p] = bits;
-        if (segmented && last)  // also the segments' first positions (no pass over the sorted keys)
-            HIDEGS_LAUNCH("radix_scatter_u64", (radix_scatter_kernel<K, true>), dim3(nt), dim3(kSBlock), 0, stream,
-                          src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals, low_base,
-                          lsd_passes == 2 ? pass_bits[0] : 0, seg_starts);
-        else
+        // narrow digits (and, for the starts, a narrower previous pass: the passes are balanced, so
+        // pass_bits[0] <= bits) take the smaller-LDS instance
+        const bool narrow = HIDEGS_SCATTER_NARROW && (int)mask < kNarrowRadix && n <= kNarrowMaxN;
+        if (segmented && last) {  // also the segments' first positions (no pass over the sorted keys)
+            const int b0 = lsd_passes == 2 ? pass_bits[0] : 0;
+            if (narrow && (1 << b0) <= kNarrowRadix)
+                HIDEGS_LAUNCH("radix_scatter_u64", (radix_scatter_kernel<K, true, kNarrowRadix>), dim3(nt), dim3(kSBlock),
+                              0, stream, src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals, low_base, b0, seg_starts);
+            else
+                HIDEGS_LAUNCH("radix_scatter_u64", (radix_scatter_kernel<K, true>), dim3(nt), dim3(kSBlock), 0, stream,
+                              src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals, low_base, b0, seg_starts);
+        } else if (narrow) {
+            HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"),
+                          (radix_scatter_kernel<K, false, kNarrowRadix>), dim3(nt), dim3(kSBlock), 0, stream, src_k, src_v,
+                          dk, dv, n, shift, mask, nt, counts, totals, nullptr, 0, nullptr);
+        } else {
             HIDEGS_LAUNCH((sizeof(K) == 8 ? "radix_scatter_u64" : "radix_scatter_u32"), (radix_scatter_kernel<K, false>),
                           dim3(nt), dim3(kSBlock), 0, stream, src_k, src_v, dk, dv, n, shift, mask, nt, counts, totals,
                           nullptr, 0, nullptr);
+        }
         src_k = dk;
         src_v = dv;
         shift += bits;
