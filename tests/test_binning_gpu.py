@@ -34,7 +34,11 @@ def raster_like_keys(K, T, seed):
     return (tiles << np.uint64(32)) | depth, np.arange(K, dtype=np.uint32)
 
 
-@pytest.mark.parametrize("K,T", [(32_768, 64), (400_000, 8160), (8_000_000, 8160), (4097, 32400), (1, 64), (2, 64)])
+# 16000 / 4000 tiles: 14 / 12 segment bits (7 + 7 / 6 + 6), so the last pass's segment starts run in the
+# 128-digit scatter instance with 7 / 6 bits before it; 12M pairs is the largest sort the 128-digit
+# instances take (kNarrowMaxN), one pair more takes the 256-digit ones
+@pytest.mark.parametrize("K,T", [(32_768, 64), (400_000, 8160), (8_000_000, 8160), (4097, 32400), (1, 64), (2, 64),
+                                 (1_000_000, 16000), (600_000, 4000), (12 << 20, 8160), ((12 << 20) + 1, 8160)])
 def test_sort_raster_keys_bit_exact(K, T):
     keys, vals = raster_like_keys(K, T, K)
     end = 32 + primitives.higher_msb(T)
