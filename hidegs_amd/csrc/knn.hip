@@ -430,7 +430,7 @@ struct KnnCounters {
 
 #ifndef HIDEGS_KNN_WAVES
 #define HIDEGS_KNN_WAVES 7  // waves per SIMD the phase-1 register budget is set for (72 VGPRs, 6 spilled to
-                           // scratch outside the evaluation loop): knn_leaf 792/790 -> 773/773 us frustum against
+                           // scratch, 28 B per lane): knn_leaf 792/790 -> 773/773 us frustum against
                            // the 6 that 79 VGPRs gave (profiles/r04_knn_waves.md)
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_KNN_WAVES))) void knn_leaf_kernel(const float4* __restrict__ sp, int P, int nleaves, int nsuper,
