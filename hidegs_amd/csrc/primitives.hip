@@ -914,6 +914,11 @@ struct BucketShared {
 // they fit together (<= kSegRun pairs), else keys and values one after the other
 static_assert(sizeof(BucketShared) >= kSegCap * sizeof(uint64_t), "staging of the keys");
 static_assert(sizeof(BucketShared) >= kSegRun * (sizeof(uint64_t) + sizeof(uint32_t)), "staging of a run");
+static_assert(sizeof(BucketShared) >= kSegCap * 2 * sizeof(uint32_t), "compact staging of a segment");
+#ifndef HIDEGS_SEG_COMPACT_STAGE
+#define HIDEGS_SEG_COMPACT_STAGE 1  // segment_sort_kernel: low halves + values staged in one pass when the
+                                    // segment's high key halves are all equal (0: keys, then values)
+#endif
 
 // ---- hot tiles: the partition queue --------------------------------------------------------
 //
@@ -2028,6 +2033,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
     uint64_t k[kSegItems];
     uint32_t v[kSegItems];
     uint32_t a = 0xffffffffu, o = 0, lo = 0xffffffffu, hi = 0;
+    // the segment's first high key half: the segment id (tile), and with no bits above end_bit -- as
+    // hidegs_sort_tile_pairs' callers guarantee -- every pair's high half; `hd` records any that differs
+    const uint32_t ref_hi = (uint32_t)(keys[begin] >> 32);
+    uint32_t hd = 0;
 #pragma unroll
     for (int q = 0; q < kSegItems; q++) {
         const uint32_t i = t + q * kBlock;
@@ -2039,6 +2048,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
             o |= x;
             lo = min(lo, x);
             hi = max(hi, x);
+            hd |= (uint32_t)(k[q] >> 32) ^ ref_hi;
         }
     }
     BucketShared& sh = lds.bucket;
@@ -2070,7 +2080,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
         const uint32_t y = __shfl_xor(mx, s, kWave);
         mx = y > mx ? y : mx;
     }
-    if (lane == 0) s_and[wave] = mx;
+    const bool wave_hd = __ballot(hd != 0u) != 0ull;
+    if (lane == 0) s_and[wave] = mx | (wave_hd ? 0x80000000u : 0u);  // mx <= kSegCap: bit 31 is free
 #pragma unroll
     for (int j = 0; j < kBuckets / kBlock; j++) {
         sh.start[t * (kBuckets / kBlock) + j] = pre;
@@ -2078,9 +2089,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
         pre += c[j];
     }
     __syncthreads();
-    uint32_t fullest = 0;
+    uint32_t fullest = 0, mixed_hi = 0;
 #pragma unroll
-    for (int w = 0; w < kWavesPerBlock; w++) fullest = s_and[w] > fullest ? s_and[w] : fullest;
+    for (int w = 0; w < kWavesPerBlock; w++) {
+        const uint32_t f = s_and[w] & 0x7fffffffu;
+        fullest = f > fullest ? f : fullest;
+        mixed_hi |= s_and[w] >> 31;
+    }
     if (fullest > (uint32_t)kMaxBucket || shift + kIndexBits > 32) {  // crowded depths, or fields too
         // wide for 32 bits: the LSD form (block-uniform branch)
         __syncthreads();
@@ -2115,6 +2130,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_S
     // 5. stage (key, value) by final position in LDS, then store the segment contiguously (stores
     //    straight from registers scatter 8- and 4-byte writes over the segment: 78 -> 50 us at 8M pairs)
     __syncthreads();
+    if (HIDEGS_SEG_COMPACT_STAGE && !mixed_hi) {
+        // one high half for the whole segment: stage the low halves and the values, (4 + 4) B per pair,
+        // so a segment of up to kSegCap pairs goes through LDS in one pass, and rebuild the keys on store
+        uint32_t* stage_lo = reinterpret_cast<uint32_t*>(&sh);
+        uint32_t* stage_vv = stage_lo + kSegCap;
+#pragma unroll
+        for (int q = 0; q < kSegItems; q++) {
+            if (t + q * kBlock < m) {
+                stage_lo[pos[q]] = (uint32_t)k[q];
+                stage_vv[pos[q]] = v[q];
+            }
+        }
+        __syncthreads();
+        const uint64_t khi = (uint64_t)ref_hi << 32;
+#pragma unroll
+        for (int q = 0; q < kSegItems; q++) {
+            const uint32_t i = t + q * kBlock;
+            if (i < m) {
+                keys[begin + i] = khi | stage_lo[i];
+                vals[begin + i] = stage_vv[i];
+            }
+        }
+        return;
+    }
     uint64_t* stage_k = reinterpret_cast<uint64_t*>(&sh);
     uint32_t* stage_v = reinterpret_cast<uint32_t*>(stage_k + kSegRun);
     const bool together = m <= (uint32_t)kSegRun;  // block-uniform
