@@ -1718,6 +1718,8 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
     uint64_t k[kSegItems];
     uint32_t v[kSegItems];
     uint32_t a = 0xffffffffu, o = 0, lo = 0xffffffffu, hi = 0;
+    const uint32_t ref_hi = (uint32_t)(src_k[begin] >> 32);  // see segment_sort_kernel
+    uint32_t hd = 0;
 #pragma unroll
     for (int q = 0; q < kSegItems; q++) {
         const uint32_t i = t + q * kBlock;
@@ -1729,6 +1731,7 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
             o |= x;
             lo = min(lo, x);
             hi = max(hi, x);
+            hd |= (uint32_t)(k[q] >> 32) ^ ref_hi;
         }
     }
     BucketShared& sh = lds.bucket;
@@ -1772,7 +1775,8 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
         const uint32_t y = __shfl_xor(mx, s, kWave);
         mx = y > mx ? y : mx;
     }
-    if (lane == 0) s_and[wave] = mx;
+    const bool wave_hd = __ballot(hd != 0u) != 0ull;
+    if (lane == 0) s_and[wave] = mx | (wave_hd ? 0x80000000u : 0u);  // mx <= kSegCap: bit 31 is free
 #pragma unroll
     for (int j = 0; j < kBuckets / kBlock; j++) {
         sh.start[t * (kBuckets / kBlock) + j] = pre;
@@ -1780,9 +1784,13 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
         pre += c[j];
     }
     __syncthreads();
-    uint32_t fullest = 0;
+    uint32_t fullest = 0, mixed_hi = 0;
 #pragma unroll
-    for (int w = 0; w < kWavesPerBlock; w++) fullest = s_and[w] > fullest ? s_and[w] : fullest;
+    for (int w = 0; w < kWavesPerBlock; w++) {
+        const uint32_t f = s_and[w] & 0x7fffffffu;
+        fullest = f > fullest ? f : fullest;
+        mixed_hi |= s_and[w] >> 31;
+    }
     if (fullest > (uint32_t)kMaxBucket || shift + kIndexBits > 32) {  // crowded depths, or fields too
         // wide for 32 bits: the LSD form (block-uniform branch)
         __syncthreads();
@@ -1817,6 +1825,28 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
     // 5. stage (key, value) by final position in LDS, then store the segment contiguously (stores
     //    straight from registers scatter 8- and 4-byte writes over the segment: 78 -> 50 us at 8M pairs)
     __syncthreads();
+    if (HIDEGS_SEG_COMPACT_STAGE && !mixed_hi) {  // one high half: low halves + values in one pass
+        uint32_t* stage_lo = reinterpret_cast<uint32_t*>(&sh);
+        uint32_t* stage_vv = stage_lo + kSegCap;
+#pragma unroll
+        for (int q = 0; q < kSegItems; q++) {
+            if (t + q * kBlock < m) {
+                stage_lo[pos[q]] = (uint32_t)k[q];
+                stage_vv[pos[q]] = v[q];
+            }
+        }
+        __syncthreads();
+        const uint64_t khi = (uint64_t)ref_hi << 32;
+#pragma unroll
+        for (int q = 0; q < kSegItems; q++) {
+            const uint32_t i = t + q * kBlock;
+            if (i < m) {
+                dk[begin + i] = khi | stage_lo[i];
+                dv[begin + i] = stage_vv[i];
+            }
+        }
+        return;
+    }
     uint64_t* stage_k = reinterpret_cast<uint64_t*>(&sh);
     uint32_t* stage_v = reinterpret_cast<uint32_t*>(stage_k + kSegRun);
     const bool together = m <= (uint32_t)kSegRun;  // block-uniform
