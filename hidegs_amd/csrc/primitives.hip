@@ -294,7 +294,8 @@ __global__ __launch_bounds__(kBlock) void radix_digit_scan_kernel(uint32_t* __re
 }
 
 // Stable scatter of one tile.  LDS: one staging buffer of the tile's keys (values reuse it
-// afterwards), per-wave digit counters -- 43 KB at 8 waves, 3 workgroups per CU.
+// afterwards), per-wave digit counters -- 43 KB at 8 waves, 3 workgroups per CU (38 KB and 4 for the
+// 128-digit instances, below).
 // Global offsets: tile_prefix[d][tile] (per-digit exclusive scan over tiles) + exclusive scan
 // of the digit totals.  (A single-pass decoupled look-back variant measured slower on MI355X:
 // the chained tile-to-tile hand-off crosses the non-coherent per-XCD L2s at every hop.)
@@ -370,6 +371,9 @@ __device__ __forceinline__ void segment_starts(const K (&k)[R], const bool (&ok)
 #define HIDEGS_SCATTER_NARROW 1
 #endif
 constexpr int kNarrowRadix = 128;
+#ifndef HIDEGS_SCATTER_NT_LOADS
+#define HIDEGS_SCATTER_NT_LOADS 0  // 1: the pass's input read with non-temporal loads (A/B builds)
+#endif
 constexpr long long kNarrowMaxN = 12ll << 20;
 template <typename K, bool Starts = false, int D = kRadix>
 __global__ __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(D == kRadix ? 1 : 8))) void radix_scatter_kernel(const K* __restrict__ keys_in,
@@ -409,8 +413,13 @@ __global__ __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(D == kR
     for (int r = 0; r < kSItems; r++) {
         const long long i = seg + r * kWave + lane;
         ok[r] = i < n;
+#if HIDEGS_SCATTER_NT_LOADS
+        k[r] = ok[r] ? __builtin_nontemporal_load(keys_in + i) : K(0);
+        v[r] = ok[r] ? __builtin_nontemporal_load(vals_in + i) : 0u;
+#else
         k[r] = ok[r] ? keys_in[i] : K(0);
         v[r] = ok[r] ? vals_in[i] : 0u;
+#endif
     }
     // the digits' global bases, scanned while the tile's loads are in flight (workgroup barriers
     // do not wait for global loads)
