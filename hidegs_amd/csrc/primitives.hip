@@ -1727,7 +1727,7 @@ __device__ __forceinline__ void sort_segment(const uint64_t* __restrict__ src_k,
     uint64_t k[kSegItems];
     uint32_t v[kSegItems];
     uint32_t a = 0xffffffffu, o = 0, lo = 0xffffffffu, hi = 0;
-    const uint32_t ref_hi = (uint32_t)(src_k[begin] >> 32);  // see segment_sort_kernel
+    const uint32_t ref_hi = m ? (uint32_t)(src_k[begin] >> 32) : 0u;  // see segment_sort_kernel (m == 0: no read)
     uint32_t hd = 0;
 #pragma unroll
     for (int q = 0; q < kSegItems; q++) {
