@@ -372,7 +372,9 @@ __device__ __forceinline__ void segment_starts(const K (&k)[R], const bool (&ok)
 #endif
 constexpr int kNarrowRadix = 128;
 #ifndef HIDEGS_SCATTER_NT_LOADS
-#define HIDEGS_SCATTER_NT_LOADS 0  // 1: the pass's input read with non-temporal loads (A/B builds)
+#define HIDEGS_SCATTER_NT_LOADS 1  // the pass's input, dead after the pass, read with non-temporal loads so it
+                                   // does not displace the output the next pass reads: scatter 42.8 -> 40.6 us
+                                   // (1080p D2 view), 4K sort 872 -> 834 us (profiles/r04_scatter_nt.md)
 #endif
 constexpr long long kNarrowMaxN = 12ll << 20;
 template <typename K, bool Starts = false, int D = kRadix>
