@@ -376,7 +376,10 @@ constexpr int kNarrowRadix = 128;
                                    // does not displace the output the next pass reads: scatter 42.8 -> 40.6 us
                                    // (1080p D2 view), 4K sort 872 -> 834 us (profiles/r04_scatter_nt.md)
 #endif
-constexpr long long kNarrowMaxN = 12ll << 20;
+#ifndef HIDEGS_NARROW_MAX_N
+#define HIDEGS_NARROW_MAX_N (12ll << 20)
+#endif
+constexpr long long kNarrowMaxN = HIDEGS_NARROW_MAX_N;
 template <typename K, bool Starts = false, int D = kRadix>
 __global__ __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(D == kRadix ? 1 : 8))) void radix_scatter_kernel(const K* __restrict__ keys_in,
                                                                 const uint32_t* __restrict__ vals_in,
