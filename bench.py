@@ -22,7 +22,8 @@ on this path is measured for real, at the configuration the metric is quoted on 
   roofline  = the dominant kernel of the step: 24 algorithmic bytes per pair per sort-pass
               launch (key 8 + value 4, read and written once), averaged over its launches with
               per-launch HIP events (hidegs_kernel_timing), against 8 TB/s; traffic from the
-              committed rocprofv3 PMC summary (profiles/latest_kernels.json).
+              committed rocprofv3 PMC summary (profiles/latest_kernels.json), with the commit and
+              source hash it was taken at (profiles/latest_kernels.meta.json).
   binning_skewed = the same step on a view whose Gaussians crowd into hot tiles (15% of them in
               a small disc: ~70 tiles over 8192 pairs take the partition queue).
   distCUDA2 = simple_knn._C.distCUDA2 on the 2M D2 centres, with its issue-rate roofline (VALU
@@ -36,9 +37,10 @@ on this path is measured for real, at the configuration the metric is quoted on 
   dp_step   = the rank's binning step + exchange_and_step, per wire format: the built part of one
               view-DP training step (views/s over all ranks; no rasterizer), for the scaling runs.
   masked Adam = the fused row-masked optimizer step at 2M Gaussians (59 fp32 each), 90% visible.
-  cpu_baseline = on rank 0 at N = 1, every CPU leg on the same `cores` threads (the box's CPU
-              share, OMP_NUM_THREADS): the oracle's OpenMP stable radix sort of the same pairs
-              (headline), its kNN brute force on sampled queries, its masked Adam step.
+  cpu_baseline = on rank 0 at N = 1, every CPU leg on the same `cores` threads (cpu_share(): the
+              CPUs the process may run on, lowered to a cgroup quota, else to the harness's declared
+              share; the evidence is in the line): the oracle's OpenMP stable radix sort of the same
+              pairs (headline), its kNN brute force on sampled queries, its masked Adam step.
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -60,7 +62,46 @@ VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2
 ROOT = os.path.dirname(os.path.abspath(__file__))
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "latest_kernels.json")  # tools/prof_summary.py output
 KNN_PMC_FILE = os.path.join(ROOT, "profiles", "latest_knn_pmc.json")   # tools/pmc_knn_valu.sh output
+TRAFFIC_META = os.path.join(ROOT, "profiles", "latest_kernels.meta.json")  # where that summary was taken
 SKEW_CLUSTER = (0.15, 0.1)
+SCOUTS = 128  # HIDEGS_SCOUTS (primitives.hip): segment_sort_kernel launches num_tiles + SCOUTS workgroups
+# the bench's kernel names (hidegs_kernel_timing) -> rocprofv3 kernel names
+ROCPROF_NAME = {"radix_scatter_u64": "radix_scatter_kernel", "segment_sort": "segment_sort_kernel",
+                "radix_hist_u64": "radix_hist_kernel", "scan_downsweep": "scan_downsweep_kernel",
+                "scan_reduce": "scan_reduce_kernel"}
+# the binning sort's kernels (every launch of hidegs_sort_tile_pairs)
+SORT_KERNELS = ("radix_hist_u64", "radix_digit_scan", "radix_scatter_u64", "segment_sort", "big_segments", "piece_sort")
+
+
+def sources_sha256() -> str:
+    """One hash over the library's kernel sources and the ABI header: identifies the code a committed
+    profile was taken on (tools/profile_note.py records it beside the profile)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "hidegs_amd", "csrc")
+    for f in sorted(os.listdir(csrc)) + ["../../include/hidegs.h"]:
+        p = os.path.join(csrc, f)
+        if os.path.isfile(p) and p.endswith((".hip", ".h", ".cpp")):
+            h.update(os.path.basename(p).encode())
+            with open(p, "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()
+
+
+def traffic_entry(dom: str, K: int, T: int, table: dict):
+    """(key, entry) of the committed rocprofv3 summary for the bench's dominant kernel: the entry of
+    the same kernel and grid (workgroups x 256 or x 512 threads), else that kernel's entry with the
+    most launches, else (None, None)."""
+    name = ROCPROF_NAME.get(dom, dom + "_kernel")
+    ntiles = (K + 4095) // 4096
+    grid = {"segment_sort": (T + SCOUTS) * 256, "radix_scatter_u64": ntiles * 512}.get(dom, ntiles * 256)
+    key = f"{name}@{grid}"
+    if key in table:
+        return key, table[key]
+    same = [(k, v) for k, v in table.items() if k.split("@")[0] == name]
+    if same:
+        return max(same, key=lambda kv: kv[1].get("launches", 0))
+    return None, None
 
 
 def free_port() -> int:
@@ -82,16 +123,58 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_threads() -> int:
-    """The CPU legs' thread count: the box's CPU share (OMP_NUM_THREADS, 16 on the GPU box), else
-    every core this process may run on."""
-    env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit() and int(env) > 0:
-        return int(env)
+def _cgroup_cpu_quota():
+    """(CPUs allowed by the cgroup CPU quota, the raw setting), or (None, setting) when unlimited or
+    unreadable: cgroup v2 cpu.max ("max 100000" / "1600000 100000"), else v1 cfs quota / period."""
+    paths = []
     try:
-        return len(os.sched_getaffinity(0))
+        for line in open("/proc/self/cgroup"):
+            _, ctrl, path = line.rstrip("\n").split(":", 2)
+            if ctrl == "":
+                paths.append(("v2", os.path.join("/sys/fs/cgroup", path.lstrip("/"), "cpu.max")))
+                paths.append(("v2", "/sys/fs/cgroup/cpu.max"))
+            elif "cpu" in ctrl.split(","):
+                for root in ("/sys/fs/cgroup/cpu,cpuacct", "/sys/fs/cgroup/cpu"):
+                    paths.append(("v1", os.path.join(root, path.lstrip("/"))))
+                    paths.append(("v1", root))
+    except OSError:
+        pass
+    for kind, p in paths:
+        try:
+            if kind == "v2":
+                raw = open(p).read().strip()
+                q, per = raw.split()
+                return (None if q == "max" else -(-int(q) // int(per))), f"{p}: {raw}"
+            q = int(open(os.path.join(p, "cpu.cfs_quota_us")).read())
+            per = int(open(os.path.join(p, "cpu.cfs_period_us")).read())
+            raw = f"{p}: cfs_quota_us {q} / cfs_period_us {per}"
+            return (None if q <= 0 else -(-q // per)), raw
+        except (OSError, ValueError):
+            continue
+    return None, "no cgroup cpu quota file readable"
+
+
+def cpu_share() -> dict:
+    """The CPU legs' thread count and its evidence (BASELINE.md §4 asks for os.cpu_count()):
+    * the CPUs this process may run on (sched_getaffinity) -- the allowed count;
+    * lowered to the cgroup CPU quota when one is set;
+    * with neither lower than os.cpu_count(), lowered to OMP_NUM_THREADS when the harness declares a
+      smaller per-GPU share there (the GPU box sets 16 and asks worker pools to stay within it)."""
+    try:
+        allowed = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        allowed = os.cpu_count() or 1
+    quota, quota_raw = _cgroup_cpu_quota()
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    omp = int(env) if env.isdigit() and int(env) > 0 else None
+    cores, source = allowed, "sched_getaffinity"
+    if quota is not None and quota < cores:
+        cores, source = quota, "cgroup cpu quota"
+    elif quota is None and omp is not None and omp < cores:
+        cores, source = omp, ("OMP_NUM_THREADS: the harness's declared per-GPU CPU share (no cgroup quota and "
+                              "no narrower affinity visible)")
+    return {"cores": cores, "cores_source": source, "sched_getaffinity": allowed, "cgroup_cpu_quota": quota,
+            "cgroup_cpu_setting": quota_raw, "omp_num_threads": omp, "host_cpu_count": os.cpu_count()}
 
 
 def parse():
@@ -291,16 +374,15 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
     dom_us = kern[dom]["avg_us"]
     dom_bytes = alg[dom]
     achieved = dom_bytes / (dom_us * 1e-6) / 1e9
-    traffic = None
-    rocprof_name = {"radix_scatter_u64": "radix_scatter_kernel", "segment_sort": "segment_sort_kernel",
-                    "radix_hist_u64": "radix_hist_kernel"}.get(dom, dom + "_kernel")
-    ntiles_sort = (K + 4095) // 4096
-    grid = {"segment_sort": (T + 16) * 256, "radix_scatter_u64": ntiles_sort * 512}.get(dom, ntiles_sort * 256)
-    traffic_src = f"{rocprof_name}@{grid}"
+    traffic, traffic_key, meta = None, None, {}
     if os.path.exists(TRAFFIC_FILE):
         with open(TRAFFIC_FILE) as f:
-            traffic = json.load(f).get(traffic_src, {}).get("hbm_bytes_per_launch")
-    sort_us = sum(kern[k]["us_per_step"] for k in kern if k.startswith(("radix_", "segment_", "big_")))
+            traffic_key, ent = traffic_entry(dom, K, T, json.load(f))
+        traffic = (ent or {}).get("hbm_bytes_per_launch")
+    if os.path.exists(TRAFFIC_META):
+        with open(TRAFFIC_META) as f:
+            meta = json.load(f)
+    sort_us = sum(kern[k]["us_per_step"] for k in kern if k in SORT_KERNELS)
     line["binning_step"] = {"ms_per_step": round(ms_step, 4), "wall_ms_per_step": round(wall_ms_step, 4),
                             "pairs_per_s_all_ranks": K * world / (ms_step * 1e-3),
                             "views_per_s_all_ranks": world / (ms_step * 1e-3),
@@ -308,8 +390,13 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
     line["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                         "traffic": None if traffic is None else round(traffic),
-                        "traffic_profile": traffic_src, "algorithmic_bytes_per_launch": dom_bytes,
-                        "avg_launch_us": dom_us}
+                        # traffic is NOT measured in this run: it is the committed PMC summary's, taken at
+                        # traffic_profile_commit on the kernel sources hashed there (same_source: this run's
+                        # sources hash the same)
+                        "traffic_profile": traffic_key, "traffic_profile_commit": meta.get("commit"),
+                        "traffic_profile_same_source": (meta.get("sources_sha256") == sources_sha256()
+                                                        if meta.get("sources_sha256") else None),
+                        "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": dom_us}
     line["ms_per_step_binning"] = round(ms_step, 4)
 
     # ---- the same step on a skewed view (hot tiles through the partition queue) ----------------
@@ -338,9 +425,10 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
         torch.cuda.synchronize()
         kk = {nm: round(kt.get(nm)[0] * 1e3, 1) for nm in ("bounds", "morton", "radix_scatter_u64", "gather",
                                                              "leaf_box", "knn_leaf", "knn_hard")}
+    # bound by the search's dependent evaluation chain (VALU issue), not HBM: 16 B/point in ~1 ms is
+    # 0.4% of the HBM peak, so no HBM fraction is reported for it -- the issue roofline below is the bound
     kd = {"points": N, "ms": round(knn_ms, 3), "points_per_s_all_ranks": N * world / (knn_ms * 1e-3),
-          "kernels_us": kk, "algorithmic_bytes": 16 * N,
-          "hbm_frac": round(16 * N / (knn_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
+          "kernels_us": kk, "algorithmic_bytes": 16 * N, "bound": "valu-issue (search latency), not HBM"}
     if os.path.exists(KNN_PMC_FILE):
         with open(KNN_PMC_FILE) as f:
             pmc = json.load(f)
@@ -415,6 +503,7 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
 
 
 def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, GradArena, ViewDPExchange):
+    import torch.distributed as dist
     g = torch.Generator(device=dev).manual_seed(rank)
     visible = torch.rand(N, device=dev, generator=g) < 0.9
     arena = GradArena(N, device=dev)
@@ -422,8 +511,21 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
     norm = torch.rand(N, 1, device=dev, generator=g)
     radii = torch.rand(N, device=dev, generator=g)
     reps = 20 if gpu else 3
+    def replicas_identical(ex) -> bool:
+        """One exchange of fresh per-rank gradients, then every rank's reduced arena compared bit for bit
+        through 1024 int64 chunk sums of its int32 view (all-gathered: 8 KB per rank)."""
+        arena.flat.normal_(generator=g)
+        ex.exchange(arena, visible, max_stats=[norm, radii])
+        flat = arena.flat.view(torch.int32)
+        pad = (-flat.numel()) % 1024
+        sums = torch.nn.functional.pad(flat, (0, pad)).view(1024, -1).to(torch.int64).sum(1)
+        got = [torch.empty_like(sums) for _ in range(world)]
+        dist.all_gather(got, sums)
+        return all(torch.equal(x, got[0]) for x in got)
+
     for transport in ("fp32", "bf16"):
         ex = ViewDPExchange(transport=transport)
+        same = replicas_identical(ex)
         ex_ms, ex_wall = timed(lambda: ex.exchange(arena, visible, max_stats=[norm, radii]), reps, 2)
         nbytes = ex.last.reduced_bytes
         algbw = nbytes / (ex_ms * 1e-3) / 1e9 if nbytes else None
@@ -436,7 +538,7 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
             "algbw_GBps": algbw,  # fp32 gradient bytes made consistent per second
             "busbw_GBps": None if algbw is None else algbw * 2 * (world - 1) / world,
             "collectives_per_step": ex.last.collectives, "compacted": ex.last.compacted,
-            "union_rows": ex.last.union_rows}
+            "union_rows": ex.last.union_rows, "replicas_bit_identical": same}
         if world == 1 and gpu:
             # the N-rank path forced on the one-rank group: every collective the multi-GPU run issues,
             # real RCCL calls (over one rank a copy), so the machinery's own cost is on the record
@@ -484,8 +586,9 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
 def _cpu_baselines(line, ctx, N, cam, np):
     import oracle
     from hidegs_amd import synthetic
-    threads = oracle.set_threads(cpu_threads())
-    info = {"cpu": cpu_model(), "cores": threads, "host_cpu_count": os.cpu_count()}
+    share = cpu_share()
+    threads = oracle.set_threads(share["cores"])
+    info = {"cpu": cpu_model(), **share, "cores": threads}
     wl, end_bit, sort_us = ctx["binning_pairs"]
     keys = wl.keys.cpu().numpy().view(np.uint64)
     vals = wl.values.cpu().numpy().view(np.uint32)

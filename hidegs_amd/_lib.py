@@ -16,7 +16,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first; libhidegs binds t
 # HIDEGS_LIB selects another build of the same ABI (tools/build_variant.py experiments)
 LIB_PATH = os.environ.get("HIDEGS_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhidegs.so")
 
-E_ARG, E_HIP, E_ALLOC, E_UNSUPPORTED = -1, -2, -3, -4
+E_ARG, E_HIP, E_ALLOC, E_UNSUPPORTED, E_ASYNC = -1, -2, -3, -4, -5
 
 P = C.c_void_p
 I = C.c_int
@@ -114,7 +114,7 @@ def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = lib().hidegs_last_error().decode(errors="replace")
         kind = {E_ARG: "bad argument", E_HIP: "HIP error", E_ALLOC: "allocation failed",
-                E_UNSUPPORTED: "unsupported"}.get(rc, f"error {rc}")
+                E_UNSUPPORTED: "unsupported", E_ASYNC: "earlier asynchronous failure"}.get(rc, f"error {rc}")
         raise RuntimeError(f"{what}: {kind}: {msg}")
 
 

@@ -7,6 +7,7 @@
 #include "common.h"
 
 #include <atomic>
+#include <mutex>
 
 namespace hidegs {
 
@@ -31,6 +32,49 @@ int check_launch(const char* stage, hipStream_t stream, int debug)
 }
 
 static int not_built(const char* fn) { return fail(HIDEGS_E_UNSUPPORTED, std::string(fn) + ": " + kNotBuilt); }
+
+namespace {
+std::once_flag g_async_once;
+uint32_t* g_async_host = nullptr;    // mapped, coherent pinned word
+uint32_t* g_async_device = nullptr;  // its device address
+}  // namespace
+
+uint32_t* async_error_slot()
+{
+    std::call_once(g_async_once, [] {
+        void* h = nullptr;
+        if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipHostFree(h);
+            return;
+        }
+        g_async_host = static_cast<uint32_t*>(h);
+        __atomic_store_n(g_async_host, 0u, __ATOMIC_SEQ_CST);
+        g_async_device = static_cast<uint32_t*>(d);
+    });
+    return g_async_device;
+}
+
+uint32_t take_async_bits()
+{
+    // the word exists only once a sort asked for its slot; before that nothing can be pending
+    return g_async_host ? __atomic_exchange_n(g_async_host, 0u, __ATOMIC_SEQ_CST) : 0u;
+}
+
+int take_async_error(const char* what)
+{
+    const uint32_t err = take_async_bits();
+    if (!err) return 0;
+    return fail(HIDEGS_E_ASYNC, std::string(what) + ": not run -- an earlier sort's hot-tile partition queue failed (error " +
+                                    std::to_string(err) + ((err & 1u) ? ", job slots exhausted" : "") +
+                                    ((err & 4u) ? ", a worker gave up waiting" : "") +
+                                    "): that sort's output is not sorted");
+}
 
 }  // namespace hidegs
 

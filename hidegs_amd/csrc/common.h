@@ -33,7 +33,19 @@ int check_launch(const char* stage, hipStream_t stream, int debug);
 bool debug_enabled();
 
 // Sticky partition-queue error word of the current device (primitives.hip); synchronises `stream`.
+// Reads and clears it in one device-side exchange.
 int queue_error(hipStream_t stream, int clear, uint32_t* flags);
+
+// Asynchronous error word: one u32 of mapped, coherent pinned host memory that a sort's last kernel
+// sets (system-scope store) when its partition queue failed, so that the failure surfaces without a
+// host synchronisation.  async_error_slot() returns its device address (NULL if it could not be
+// allocated: then only the debug mode and hidegs_queue_error report queue errors).
+uint32_t* async_error_slot();
+// Called first by every compute entry point: a set word is taken (exchanged with 0) and turned into
+// HIDEGS_E_ASYNC with its message, so the call after a failed sort fails loudly instead of running.
+int take_async_error(const char* what);
+// The word's bits, taken (exchanged with 0); 0 when none are pending.
+uint32_t take_async_bits();
 
 // 256-byte aligned carving of one caller-provided scratch buffer.
 constexpr size_t kAlign = 256;

@@ -2463,10 +2463,16 @@ __global__ __launch_bounds__(kBlock) void big_segment_kernel(uint64_t* __restric
 constexpr int kPieceBlocks = 256 * HIDEGS_PIECE_WAVES;  // one workgroup per resident slot
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_PIECE_WAVES))) void piece_sort_kernel(
     uint64_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint64_t* __restrict__ alt_k,
-    const uint32_t* __restrict__ alt_v, const BigQueue q)
+    const uint32_t* __restrict__ alt_v, const BigQueue q, uint32_t* async_err)
 {
     __shared__ __attribute__((aligned(16))) SegLds lds;
     __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock], s_max[kWavesPerBlock];
+    // the queue has drained (stream order): its error word is final.  A set word goes to the mapped
+    // host word (a vector store at system scope), which the next entry-point call takes as HIDEGS_E_ASYNC.
+    if (async_err && blockIdx.x == 0 && threadIdx.x == 0) {
+        const uint32_t err = q_peek(&q.ctl[kCtlStride * Q_ERROR]);
+        if (err) __hip_atomic_store(async_err, err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     const uint32_t np = min(q.ctl[kCtlStride * Q_NPIECE], q.piece_cap);
     for (uint32_t p = blockIdx.x; p < np; p += gridDim.x) {
         const uint2 e = q.piece[p];
@@ -2707,13 +2713,20 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
                       vals_out, seg_starts, ranges_out, nseg, q);
         HIDEGS_LAUNCH("big_segments", big_segment_kernel, dim3(kQueueBlocks), dim3(kBlock), 0, stream, ko, vals_out,
                       reinterpret_cast<uint64_t*>(alt_k), alt_v, q);
-        if (kDeferPieces)
-            HIDEGS_LAUNCH("piece_sort", piece_sort_kernel, dim3(kPieceBlocks), dim3(kBlock), 0, stream, ko, vals_out,
-                          reinterpret_cast<const uint64_t*>(alt_k), alt_v, q);
-        if (debug_enabled()) {  // debug mode: the queue's own error word, after the grid has drained
+        // debug mode checks this call's queue itself (below); otherwise the last kernel hands a queue
+        // error to the mapped host word, which fails the next entry-point call
+        const bool debug = debug_enabled();
+        uint32_t* async_err = debug ? nullptr : async_error_slot();
+        static_assert(kDeferPieces, "piece_sort_kernel is the sort's last kernel: it reports the queue's error");
+        HIDEGS_LAUNCH("piece_sort", piece_sort_kernel, dim3(kPieceBlocks), dim3(kBlock), 0, stream, ko, vals_out,
+                      reinterpret_cast<const uint64_t*>(alt_k), alt_v, q, async_err);
+        if (debug) {  // debug mode: this call's own queue error word (in its scratch), after the grid has drained
             if (int rc = check_launch(what, stream, 1)) return rc;
             uint32_t err = 0;
-            if (int rc = queue_error(stream, 1, &err)) return rc;
+            if (hipMemcpyAsync(&err, q.ctl + kCtlStride * Q_ERROR, sizeof(err), hipMemcpyDeviceToHost, stream) !=
+                    hipSuccess ||
+                hipStreamSynchronize(stream) != hipSuccess)
+                return fail(HIDEGS_E_HIP, std::string(what) + ": queue error readback failed");
             if (err)
                 return fail(HIDEGS_E_HIP, std::string(what) + ": hot-tile partition queue error " + std::to_string(err) +
                                               ((err & 1u) ? " (job slots exhausted)" : "") +
@@ -2730,17 +2743,24 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
 
 }  // namespace
 
+// Reads (clear: exchanges with 0) the sticky word in one device-side atomic, so an error raised
+// between a read and a separate clear cannot be lost.
+__device__ uint32_t g_queue_error_read;
+__global__ void queue_error_take_kernel(int clear)
+{
+    g_queue_error_read = clear ? __hip_atomic_exchange(&g_queue_error, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : __hip_atomic_load(&g_queue_error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 int queue_error(hipStream_t stream, int clear, uint32_t* flags)
 {
     uint32_t v = 0;
-    if (hipStreamSynchronize(stream) != hipSuccess ||
-        hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_queue_error), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess)
+    hipLaunchKernelGGL(queue_error_take_kernel, dim3(1), dim3(1), 0, stream, clear);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(stream) != hipSuccess ||
+        hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_queue_error_read), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess)
         return fail(HIDEGS_E_HIP, "queue_error: readback failed");
-    if (clear && v) {
-        const uint32_t z = 0;
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_queue_error), &z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
-            return fail(HIDEGS_E_HIP, "queue_error: clear failed");
-    }
+    // the asynchronous copy of the same failures: reported here and taken with the clear
+    if (clear) v |= take_async_bits();
     *flags = v;
     return 0;
 }
@@ -2811,6 +2831,7 @@ size_t hidegs_scan_scratch_bytes(long long n) { return n > 0 ? hidegs::inclusive
 int hidegs_inclusive_scan_u32(void* scratch, size_t scratch_bytes, const uint32_t* in, uint32_t* out, long long n,
                               void* stream)
 {
+    if (int rc = hidegs::take_async_error("hidegs_inclusive_scan_u32")) return rc;
     return hidegs::inclusive_scan_u32(scratch, scratch_bytes, in, out, n, hidegs::as_stream(stream));
 }
 
@@ -2819,6 +2840,7 @@ int hidegs_sort_pairs_u64(void* scratch, size_t scratch_bytes, const uint64_t* k
                           const uint32_t* vals_in, uint32_t* vals_out, long long n, int begin_bit, int end_bit,
                           void* stream)
 {
+    if (int rc = hidegs::take_async_error("hidegs_sort_pairs_u64")) return rc;
     return hidegs::sort_pairs_u64(scratch, scratch_bytes, keys_in, keys_out, vals_in, vals_out, n, begin_bit, end_bit,
                                   hidegs::as_stream(stream));
 }
@@ -2828,6 +2850,7 @@ int hidegs_sort_pairs_u32(void* scratch, size_t scratch_bytes, const uint32_t* k
                           const uint32_t* vals_in, uint32_t* vals_out, long long n, int begin_bit, int end_bit,
                           void* stream)
 {
+    if (int rc = hidegs::take_async_error("hidegs_sort_pairs_u32")) return rc;
     return hidegs::sort_pairs_u32(scratch, scratch_bytes, keys_in, keys_out, vals_in, vals_out, n, begin_bit, end_bit,
                                   hidegs::as_stream(stream));
 }
@@ -2836,6 +2859,7 @@ int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* 
                            const uint32_t* vals_in, uint32_t* vals_out, long long n, int num_tiles, uint32_t* ranges,
                            void* stream)
 {
+    if (int rc = hidegs::take_async_error("hidegs_sort_tile_pairs")) return rc;
     return hidegs::sort_tile_pairs(scratch, scratch_bytes, keys_in, keys_out, vals_in, vals_out, n, num_tiles, ranges,
                                    hidegs::as_stream(stream));
 }
@@ -2843,6 +2867,7 @@ int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* 
 int hidegs_identify_tile_ranges(const uint64_t* sorted_keys, long long n, uint32_t* ranges, int num_tiles,
                                 void* stream)
 {
+    if (int rc = hidegs::take_async_error("hidegs_identify_tile_ranges")) return rc;
     return hidegs::identify_tile_ranges(sorted_keys, n, ranges, num_tiles, hidegs::as_stream(stream));
 }
 

@@ -38,7 +38,13 @@ fp32 in rank order (0, 1, ...) and rounds the sum to bf16 once; one all-gather r
 sum to every rank.  The result is each element's bf16(sum_r bf16(g_r)) -- within ~2^-8 relative of the
 fp32 sum per input plus one output rounding, identical on every rank (each chunk is summed by exactly
 one rank, in a fixed order), so the replicas stay bit-identical.  It is a semantic change (SURVEY §8(e)
-E2 item 3: "bf16 transport, behind a parity flag"); the default stays fp32.
+E2 item 3: "bf16 transport, behind a parity flag"); the default stays fp32, and stays so until an N > 1
+measurement shows the halved xGMI bytes save more than the wire's local cost (pack, sum, unpack and
+twice the collectives: +0.73 ms per 472 MB step on the forced one-rank RCCL path, BENCH_r04).
+Memory: a bf16 bucket in flight holds a send, a receive and a gathered buffer of 2 B per element each
+(and its rank's chunk sum); at most `BF16_IN_FLIGHT` buckets are started ahead of the one being
+finished, so the extra memory is bounded by (BF16_IN_FLIGHT + 1) x 6 B x bucket elements (~480 MB at
+the default 64 MiB buckets) whatever the arena's size, instead of ~6 B per arena element.
 
 `exchange_and_step` fuses the exchange with the masked optimizer step that follows it: each
 dense bucket's rows are updated as soon as that bucket's all-reduce lands, while the later
@@ -143,6 +149,7 @@ class ExchangeStats:
 
 
 TRANSPORTS = ("fp32", "bf16")
+BF16_IN_FLIGHT = 4  # bf16 buckets started ahead of the one being finished (bounds the wire buffers' memory)
 
 
 class _Bucket:
@@ -186,8 +193,10 @@ class _Bucket:
                 acc += parts[r].to(torch.float32)
             mine = acc.to(torch.bfloat16)
         self.gathered = torch.empty_like(self.send)
+        self.send = self.recv = None  # the all-to-all is complete and `mine` is formed: free them now
         self.work = dist.all_gather_into_tensor(self.gathered.view(torch.uint8), mine.view(torch.uint8),
                                                 group=self.group, async_op=True)
+        self.mine = mine  # kept alive until the all-gather is waited on
         return 1
 
     def finish(self) -> None:
@@ -198,7 +207,7 @@ class _Bucket:
                 wire.bf16_unpack(self.gathered, flat)
             else:
                 flat.copy_(self.gathered[:self.view.numel()])
-            self.send = self.recv = self.gathered = None
+            self.gathered = self.mine = None
 
     @property
     def wire_bytes(self) -> int:
@@ -261,16 +270,27 @@ class ViewDPExchange:
         return _Bucket(view, self.group, self.transport, dist.get_world_size(self.group), dist.get_rank(self.group))
 
     def _run_buckets(self, buckets: List[_Bucket], after=None) -> None:
-        """Every bucket's first collective issued at once, then per bucket in order: its second
-        collective (bf16) issued one bucket ahead, its wait, and `after(i)` (e.g. that bucket's rows'
-        optimizer update) while the later buckets are still on the wire."""
-        for b in buckets:
-            self.last.collectives += b.start()
-            self.last.wire_bytes += b.wire_bytes
-            self.last.reduced_bytes += b.view.numel() * 4
+        """fp32: every bucket's all-reduce issued at once (in place: no extra memory).  bf16: the first
+        collective of up to BF16_IN_FLIGHT buckets ahead of the one being finished.  Then per bucket in
+        order: its second collective (bf16) issued one bucket ahead, its wait, and `after(i)` (e.g. that
+        bucket's rows' optimizer update) while the later buckets are still on the wire."""
+        ahead = len(buckets) if self.transport == "fp32" else max(2, BF16_IN_FLIGHT)
+        started = 0
+
+        def start_until(k):
+            nonlocal started
+            while started < min(k, len(buckets)):
+                b = buckets[started]
+                self.last.collectives += b.start()
+                self.last.wire_bytes += b.wire_bytes
+                self.last.reduced_bytes += b.view.numel() * 4
+                started += 1
+
+        start_until(ahead)
         if buckets:
             self.last.collectives += buckets[0].mid()
         for i, b in enumerate(buckets):
+            start_until(i + 1 + ahead)
             if i + 1 < len(buckets):
                 self.last.collectives += buckets[i + 1].mid()
             b.finish()

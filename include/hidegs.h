@@ -45,6 +45,9 @@ extern "C" {
 #define HIDEGS_E_HIP (-2)         /* HIP runtime or kernel error */
 #define HIDEGS_E_ALLOC (-3)       /* a buffer callback returned NULL for a non-zero request */
 #define HIDEGS_E_UNSUPPORTED (-4) /* entry point not built in this release */
+#define HIDEGS_E_ASYNC (-5)       /* not run: an earlier call's asynchronous check failed (a sort's partition
+                                     queue; see hidegs_queue_error) -- the reference's fail-fast contract
+                                     without a host synchronisation per sort */
 
 /*
  * Scratch allocator callback, the C form of the reference's std::function<char*(size_t)>
@@ -159,8 +162,12 @@ int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* 
  * [host] Error word of the hot-tile partition queue inside hidegs_sort_pairs_u64 /
  * hidegs_sort_tile_pairs, sticky per device since it was last cleared: bit 1 = job slots
  * exhausted, bit 4 = a queue worker gave up waiting.  Non-zero means some sort since the last
- * clear returned pairs that are not fully sorted.  Synchronises `stream`; clear != 0 resets it.
- * In debug mode (hidegs_set_debug) every such sort checks it itself and returns HIDEGS_E_HIP.
+ * clear returned pairs that are not fully sorted.  Synchronises `stream`; clear != 0 resets it (one
+ * device-side exchange, so no error raised meanwhile is lost) and also takes the asynchronous word below.
+ * Outside debug mode a failing sort also sets a process-wide word in mapped host memory from its last
+ * kernel; the next call of any compute entry point finds it set, clears it and returns HIDEGS_E_ASYNC
+ * without running (no host synchronisation per sort).  In debug mode (hidegs_set_debug) every such
+ * sort checks its own queue after synchronising and returns HIDEGS_E_HIP itself.
  */
 int hidegs_queue_error(void* stream, int clear, uint32_t* flags);
 

@@ -31,6 +31,22 @@ def test_header_parses():
     assert len(fns) == 28
 
 
+def test_error_codes_match_header():
+    """The HIDEGS_E_* codes of include/hidegs.h are the ones the binding maps to messages."""
+    codes = {m.group(1): int(m.group(2)) for m in
+             re.finditer(r"#define HIDEGS_E_(\w+)\s+\((-?\d+)\)", open(HEADER).read())}
+    assert codes == {"ARG": _lib.E_ARG, "HIP": _lib.E_HIP, "ALLOC": _lib.E_ALLOC, "UNSUPPORTED": _lib.E_UNSUPPORTED,
+                     "ASYNC": _lib.E_ASYNC}
+    with pytest.raises(RuntimeError, match="earlier asynchronous failure"):
+        _lib.check(_lib.E_ASYNC, "sort_tile_pairs")
+
+
+def test_no_async_error_pending_without_a_device(built_lib):
+    """No sort has run, so no asynchronous error word exists: entry points go on to validate their
+    arguments (and hidegs_queue_error is the only reader that synchronises)."""
+    assert built_lib.hidegs_inclusive_scan_u32(None, 0, None, None, 0, None) == 0
+
+
 def test_every_header_symbol_exported(built_lib):
     for name in header_functions():
         assert hasattr(built_lib, name), name

@@ -476,9 +476,12 @@ def test_one_workgroup_global_form_variant():
 
 def test_queue_overflow_is_reported_not_silent():
     """A build whose partition queue holds 64 job slots (build.VARIANTS['qcap']) cannot queue a 300K-pair
-    hot tile's jobs: the sort must report it -- through the sticky error word (hidegs_queue_error),
-    and in debug mode as the call's own HIDEGS_E_HIP -- rather than return a mis-sorted tile silently.
-    The product build sorts the same input correctly with the word clear."""
+    hot tile's jobs: the sort must report it rather than return a mis-sorted tile silently.
+    * product mode (debug off): the failing call returns 0 (no host sync), its last kernel sets the
+      mapped host word, and the NEXT call of any entry point fails with HIDEGS_E_ASYNC without running;
+      the sticky device word (hidegs_queue_error) holds the bit until cleared;
+    * debug mode: the call itself returns HIDEGS_E_HIP from its own queue's word.
+    The product build sorts the same input correctly with the words clear."""
     import ctypes as C
 
     from hidegs_amd import _lib, build
@@ -501,8 +504,28 @@ def test_queue_overflow_is_reported_not_silent():
     assert var.hidegs_queue_error(stream, 1, C.byref(flags)) == 0
     rc, _ = run()
     assert rc == 0  # without debug mode the call itself cannot know (no host sync) ...
+    torch.cuda.synchronize()
+    # ... but the next call of any entry point does, and refuses to run
+    x = torch.ones(1000, dtype=torch.int32, device=kd.device)
+    tmp = torch.empty(var.hidegs_scan_scratch_bytes(1000), dtype=torch.uint8, device=kd.device)
+    rc = var.hidegs_inclusive_scan_u32(tmp.data_ptr(), tmp.numel(), x.data_ptr(), x.data_ptr(), 1000, stream)
+    assert rc == _lib.E_ASYNC
+    msg = var.hidegs_last_error()
+    assert b"job slots exhausted" in msg and b"not run" in msg
+    assert torch.equal(x.cpu(), torch.ones(1000, dtype=torch.int32))  # it did not run
+    # the word was taken: the call after that runs
+    assert var.hidegs_inclusive_scan_u32(tmp.data_ptr(), tmp.numel(), x.data_ptr(), x.data_ptr(), 1000, stream) == 0
+    assert int(x[-1]) == 1000
+    # the sticky device word still holds the failure until it is read and cleared
     assert var.hidegs_queue_error(stream, 1, C.byref(flags)) == 0
-    assert flags.value & 1, "job-slot overflow not reported"  # ... but the sticky word does
+    assert flags.value & 1, "job-slot overflow not reported"
+    assert var.hidegs_queue_error(stream, 1, C.byref(flags)) == 0 and flags.value == 0
+    # hidegs_queue_error's clear also takes a pending asynchronous word
+    rc, _ = run()
+    assert rc == 0
+    assert var.hidegs_queue_error(stream, 1, C.byref(flags)) == 0 and flags.value & 1
+    rc = var.hidegs_inclusive_scan_u32(tmp.data_ptr(), tmp.numel(), x.data_ptr(), x.data_ptr(), 1000, stream)
+    assert rc == 0
     var.hidegs_set_debug(1)
     try:
         rc, _ = run()
@@ -510,12 +533,16 @@ def test_queue_overflow_is_reported_not_silent():
         assert b"job slots exhausted" in var.hidegs_last_error()
     finally:
         var.hidegs_set_debug(0)
-    # the debug-mode check reported the error through the call and consumed the sticky word
-    assert var.hidegs_queue_error(stream, 1, C.byref(flags)) == 0 and flags.value == 0
+    # debug mode reports through the call and leaves no asynchronous word behind; the sticky word is
+    # the device's history and keeps the bit until cleared
+    rc = var.hidegs_inclusive_scan_u32(tmp.data_ptr(), tmp.numel(), x.data_ptr(), x.data_ptr(), 1000, stream)
+    assert rc == 0
+    assert var.hidegs_queue_error(stream, 1, C.byref(flags)) == 0 and flags.value & 1
     # the product build: same input, sorted correctly, word clear (checked by the fixture too)
     ek, ev = binning.stable_sort_pairs(keys, vals, 0, 32 + primitives.higher_msb(T))
     _, vo, _ = primitives.sort_tile_pairs(kd, vd, T)
     assert np.array_equal(vo.cpu().numpy().view(np.uint32), ev)
+    assert primitives.queue_error() == 0
 
 
 def test_debug_mode_passes_clean_sorts():

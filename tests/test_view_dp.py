@@ -1,4 +1,4 @@
-"""View-data-parallel exchange over gloo, world sizes 2 and 3, on CPU.
+"""View-data-parallel exchange over gloo, world sizes 2, 3, 4 and 8, on CPU.
 
 Each rank builds synthetic per-view gradients with its own visibility mask (rows a view
 does not see are zero, as the rasterizer's backward produces them), runs the exchange for
@@ -21,9 +21,17 @@ N = 1000
 STEPS = 3
 
 
-def rank_inputs(rank, step, n=N):
+def rank_inputs(rank, step, n=N, pattern="rate"):
+    """pattern "rate": rank r sees a random 30 + 10r % of the rows (the union nearly all rows at world >= 4);
+    "window": rank r sees 90% of the rows in [r n/16, r n/16 + n/4) -- divergent views whose union over 8
+    ranks is 11/16 of the rows, so the exchange compacts at world 8."""
     g = torch.Generator().manual_seed(1234 + 97 * rank + 7919 * step)
-    visible = torch.rand(n, generator=g) < (0.3 + 0.1 * rank)
+    if pattern == "window":
+        rows = torch.arange(n)
+        lo = rank * n // 16
+        visible = (rows >= lo) & (rows < lo + n // 4) & (torch.rand(n, generator=g) < 0.9)
+    else:
+        visible = torch.rand(n, generator=g) < (0.3 + 0.1 * rank)
     grads = {}
     for name, w in LEAF_WIDTHS.items():
         t = torch.randn(n, w, generator=g)
@@ -47,7 +55,7 @@ def free_port():
     return port
 
 
-def worker(rank, world, port, compact_below, bucket_bytes, use_arena, q):
+def worker(rank, world, port, compact_below, bucket_bytes, use_arena, q, pattern="rate"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -57,7 +65,7 @@ def worker(rank, world, port, compact_below, bucket_bytes, use_arena, q):
         e_accum, e_denom, e_radii = initial_state()
         ok, err, info = True, 0.0, None
         for step in range(STEPS):
-            visible, grads, norm, radii = rank_inputs(rank, step)
+            visible, grads, norm, radii = rank_inputs(rank, step, pattern=pattern)
             if use_arena:
                 arena = GradArena(N)
                 for k, v in grads.items():
@@ -72,7 +80,7 @@ def worker(rank, world, port, compact_below, bucket_bytes, use_arena, q):
             denom += res.view_count
             max_radii = torch.maximum(max_radii, radii)
             # expected: the world's views applied one after another (reference semantics)
-            all_in = [rank_inputs(r, step) for r in range(world)]
+            all_in = [rank_inputs(r, step, pattern=pattern) for r in range(world)]
             exp_union = torch.zeros(N, dtype=torch.bool)
             for v, g, nv, rv in all_in:
                 exp_union |= v
@@ -84,6 +92,11 @@ def worker(rank, world, port, compact_below, bucket_bytes, use_arena, q):
                 err = max(err, float((reduced[name] - exp).abs().max()))
             ok = ok and torch.equal(res.union, exp_union) and torch.equal(accum, e_accum) \
                 and torch.equal(denom, e_denom) and torch.equal(max_radii, e_radii)
+            # replicas bit-identical: every rank's reduced gradients and replicated state
+            mine = torch.cat([reduced[k].reshape(-1) for k in LEAF_WIDTHS] + [accum.reshape(-1), denom.reshape(-1)])
+            got = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(got, mine)
+            ok = ok and all(torch.equal(x.view(torch.int32), got[0].view(torch.int32)) for x in got)
             info = (ex.last.union_rows, ex.last.collectives, ex.last.compacted, int(exp_union.sum()))
         if rank == 0:
             q.put((ok and err < 1e-5, err, info))
@@ -91,11 +104,11 @@ def worker(rank, world, port, compact_below, bucket_bytes, use_arena, q):
         dist.destroy_process_group()
 
 
-def run(world, compact_below, bucket_bytes, use_arena):
+def run(world, compact_below, bucket_bytes, use_arena, pattern="rate"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, world, port, compact_below, bucket_bytes, use_arena, q))
+    procs = [ctx.Process(target=worker, args=(r, world, port, compact_below, bucket_bytes, use_arena, q, pattern))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -105,18 +118,24 @@ def run(world, compact_below, bucket_bytes, use_arena):
     return q.get(timeout=10)
 
 
-@pytest.mark.parametrize("world,compact_below,bucket_bytes,use_arena", [
-    (2, 1.0, 64 << 20, True),    # compacted (union < 100% of rows)
-    (2, 0.0, 64 << 20, True),    # dense, in place on the arena
-    (2, 0.0, 64 << 20, False),   # dense, separate tensors
-    (2, 1.0, 4096, False),       # compacted, many buckets
-    (3, 1.0, 1000, True),
+@pytest.mark.parametrize("world,compact_below,bucket_bytes,use_arena,pattern,compacts", [
+    (2, 1.0, 64 << 20, True, "rate", True),    # compacted (union < 100% of rows)
+    (2, 0.0, 64 << 20, True, "rate", False),   # dense, in place on the arena
+    (2, 0.0, 64 << 20, False, "rate", False),  # dense, separate tensors
+    (2, 1.0, 4096, False, "rate", True),       # compacted, many buckets
+    (3, 1.0, 1000, True, "rate", True),
+    # world 8 (the driver's scaling node): divergent windows, union 11/16 < the default 0.75 -> compacted
+    (8, 0.75, 4096, True, "window", True),
+    (8, 0.0, 4096, True, "window", False),     # the same views, dense
+    (8, 0.75, 64 << 20, True, "rate", False),  # union ~ all rows: the default stays dense
 ])
-def test_multistep_exchange_matches_sequential_reference(world, compact_below, bucket_bytes, use_arena):
-    ok, err, (union_rows, collectives, compacted, exp_rows) = run(world, compact_below, bucket_bytes, use_arena)
-    assert ok, f"max grad error {err}"
+def test_multistep_exchange_matches_sequential_reference(world, compact_below, bucket_bytes, use_arena, pattern,
+                                                         compacts):
+    ok, err, (union_rows, collectives, compacted, exp_rows) = run(world, compact_below, bucket_bytes, use_arena,
+                                                                  pattern)
+    assert ok, f"max grad error {err} (or replicas differ)"
     assert union_rows == exp_rows
-    assert compacted == (compact_below == 1.0)
+    assert compacted == compacts
     # one all-gather (masks) + SUM buckets + ONE fused MAX
     nbytes = 4 * 59 * (exp_rows if compacted else N)
     assert collectives == 1 + -(-nbytes // bucket_bytes) + 1
@@ -270,6 +289,8 @@ def run_step(world, compact_below, bucket_bytes, transport="fp32"):
     (2, 0.0, 4096, "rows", "bf16"),       # bf16 wire: all-to-all + all-gather per bucket, pipelined
     (3, 0.0, 1 << 20, "rows", "bf16"),
     (3, 1.0, 4096, "whole", "bf16"),
+    (8, 0.0, 4096, "rows", "fp32"),       # world 8: per-bucket overlap at the driver's scaling width
+    (8, 0.0, 4096, "rows", "bf16"),
 ])
 def test_exchange_and_step_steps_each_row_once_after_its_reduction(world, compact_below, bucket_bytes, mode, transport):
     ok, got_mode, collectives = run_step(world, compact_below, bucket_bytes, transport)
@@ -287,7 +308,7 @@ def bf16_sum(parts):
     return acc.to(torch.bfloat16).to(torch.float32)
 
 
-def worker_bf16(rank, world, port, compact_below, bucket_bytes, q):
+def worker_bf16(rank, world, port, compact_below, bucket_bytes, q, pattern="rate"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -295,12 +316,12 @@ def worker_bf16(rank, world, port, compact_below, bucket_bytes, q):
         ex = ViewDPExchange(bucket_bytes=bucket_bytes, compact_below=compact_below, transport="bf16")
         ok, rel = True, 0.0
         for step in range(2):
-            visible, grads, norm, _ = rank_inputs(rank, step)
+            visible, grads, norm, _ = rank_inputs(rank, step, pattern=pattern)
             arena = GradArena(N)
             for k, v in grads.items():
                 arena[k].copy_(v)
             ex.exchange(arena, visible, max_stats=[norm])
-            all_in = [rank_inputs(r, step) for r in range(world)]
+            all_in = [rank_inputs(r, step, pattern=pattern) for r in range(world)]
             for k in LEAF_WIDTHS:
                 parts = [a[1][k] for a in all_in]
                 ok = ok and torch.equal(arena[k], bf16_sum(parts))  # the definition, bit for bit
@@ -317,16 +338,18 @@ def worker_bf16(rank, world, port, compact_below, bucket_bytes, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,compact_below,bucket_bytes", [(2, 0.0, 64 << 20), (3, 0.0, 4096), (3, 1.0, 1000),
-                                                              (4, 0.0, 10000)])
-def test_bf16_transport_is_its_definition_and_identical_on_every_rank(world, compact_below, bucket_bytes):
+@pytest.mark.parametrize("world,compact_below,bucket_bytes,pattern", [
+    (2, 0.0, 64 << 20, "rate"), (3, 0.0, 4096, "rate"), (3, 1.0, 1000, "rate"), (4, 0.0, 10000, "rate"),
+    (8, 0.75, 4096, "window"),  # world 8, divergent views: compacted, [world][chunk] wire layout at 8 ranks
+    (8, 0.0, 10000, "window")])
+def test_bf16_transport_is_its_definition_and_identical_on_every_rank(world, compact_below, bucket_bytes, pattern):
     """transport="bf16": half the wire bytes, the sum formed in fp32 by the chunk's owner; the result
     equals bf16(sum_r bf16(g_r)) exactly and is the same on every rank; within 2^-7 of the exact sum
     relative to sum_r |g_r| (two bf16 roundings of relative 2^-9 each, plus fp32 adds)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker_bf16, args=(r, world, port, compact_below, bucket_bytes, q))
+    procs = [ctx.Process(target=worker_bf16, args=(r, world, port, compact_below, bucket_bytes, q, pattern))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -336,7 +359,7 @@ def test_bf16_transport_is_its_definition_and_identical_on_every_rank(world, com
     ok, rel, wire, reduced, compacted = q.get(timeout=10)
     assert ok, "bf16 exchange differs from its definition or between ranks"
     assert rel <= 2.0 ** -7, rel
-    assert wire * 2 == reduced and compacted == (compact_below == 1.0)
+    assert wire * 2 == reduced and compacted == (compact_below > 0.0)
 
 
 def test_transport_is_checked():

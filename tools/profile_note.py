@@ -1,5 +1,7 @@
 """Write profiles/<NAME>.md, <NAME>_bench.json, <NAME>_kernels.json, <NAME>_kernel_stats.csv and refresh
-profiles/latest_kernels.json / latest_knn_pmc.json from a tools/gpu_round4.sh run in gpurun_out/.
+profiles/latest_kernels.json / latest_knn_pmc.json (+ latest_kernels.meta.json: the commit and the kernel
+sources' hash the profile was taken on, which bench.py reports beside the traffic it reads) from a
+tools/gpu_round5.sh run in gpurun_out/.
 
 usage: python tools/profile_note.py NAME "title" "command / commit note"
 """
@@ -21,6 +23,17 @@ def main():
                             os.path.join(G, "prof_fetch"), os.path.join(G, "prof_write")], check=True, capture_output=True,
                            text=True, env=dict(os.environ, PROF_JSON=kj)).stdout
     shutil.copy(kj, os.path.join(P, "latest_kernels.json"))
+    sys.path.insert(0, ROOT)
+    import bench
+    head = subprocess.run(["git", "rev-parse", "HEAD"], cwd=ROOT, capture_output=True, text=True).stdout.strip()
+    dirty = subprocess.run(["git", "status", "--porcelain", "hidegs_amd/csrc", "include"], cwd=ROOT,
+                           capture_output=True, text=True).stdout.strip() != ""
+    box_sha = os.path.join(G, "sources.sha256")  # written on the GPU box by the session script
+    sha = open(box_sha).read().strip() if os.path.exists(box_sha) else bench.sources_sha256()
+    with open(os.path.join(P, "latest_kernels.meta.json"), "w") as f:
+        json.dump({"commit": head[:12] + ("+uncommitted kernel edits" if dirty else ""), "sources_sha256": sha,
+                   "profile": name, "command": "tools/gpu_round5.sh: rocprofv3 --kernel-trace --stats, then "
+                   "--pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py", "note": note}, f, indent=1)
     shutil.copy(os.path.join(G, "prof_kt", "kt_kernel_stats.csv"), os.path.join(P, f"{name}_kernel_stats.csv"))
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_json.py"), os.path.join(G, "prof_knn"),
                     os.path.join(P, "latest_knn_pmc.json"), "knn_leaf"], check=True, capture_output=True)
@@ -32,7 +45,7 @@ def main():
     tests = open(os.path.join(G, "gputest.log")).read().strip().splitlines()[-1]
     with open(os.path.join(P, f"{name}.md"), "w") as f:
         f.write(f"# {title}\n\n")
-        f.write(f"Command: `tools/gpu_round4.sh` ({note}; tests: {tests}; smoke; bench; rocprofv3 kernel trace; "
+        f.write(f"Command: `tools/gpu_round5.sh` ({note}; tests: {tests}; smoke; bench; rocprofv3 kernel trace; "
                 "FETCH_SIZE / WRITE_SIZE passes; knn VALU pass).\n")
         f.write(f"Bench line: `{name}_bench.json`: binning step {b['ms_per_step']} ms (radix_scatter {r['avg_launch_us']} us "
                 f"in-bench = {r['frac']} of 8 TB/s; traffic {r['traffic'] / 1e6:.1f} MB against "
