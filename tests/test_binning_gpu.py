@@ -625,6 +625,57 @@ def test_one_tile_of_36m_pairs_properties():
 
 
 
+def test_sort_tile_pairs_at_the_maximum_size():
+    """n = 2^31 - 1 pairs, the ABI's largest sort (positions and counts are u32, n < 2^31), over the 1080p
+    grid's 8160 tiles with heavily repeated depths and one hot tile of 2^26 pairs (the partition queue at
+    scale).  Checked by size-independent properties: the output holds the input's pairs (keys[vo] == ko,
+    vo a permutation), in key order with equal keys in input order, and the ranges are the tiles' counts
+    laid end to end."""
+    n, T = (1 << 31) - 1, 8160
+    gen = torch.Generator(device="cuda").manual_seed(31)
+    tiles = torch.randint(0, T, (n,), device="cuda", generator=gen, dtype=torch.int64)
+    tiles[torch.randint(0, n, (1 << 26,), device="cuda", generator=gen)] = 4321
+    depth = torch.randint(0, 100_000, (n,), device="cuda", generator=gen, dtype=torch.int32)
+    depth = (depth.float() * 1e-3 + 0.2).view(torch.int32).to(torch.int64)
+    keys = (tiles << 32) | depth
+    del depth
+    counts = torch.bincount(tiles, minlength=T)
+    del tiles
+    vals = torch.arange(n, dtype=torch.int32, device="cuda")
+    ko, vo, r = primitives.sort_tile_pairs(keys, vals, T)
+    assert primitives.queue_error() == 0
+    vl = vo.long()
+    assert torch.equal(keys[vl], ko)
+    del keys
+    seen = torch.zeros(n, dtype=torch.bool, device="cuda")
+    seen[vl] = True
+    assert bool(seen.all())
+    del seen, vl
+    dk = ko[1:] - ko[:-1]  # tiles < 2^13: the keys are positive int64, no overflow
+    assert bool((dk >= 0).all())
+    tie = dk == 0
+    del dk
+    assert bool((vo[1:][tie] > vo[:-1][tie]).all())
+    del tie
+    start = torch.cumsum(counts, 0) - counts
+    rr = r.long()
+    present = counts > 0
+    assert torch.equal(rr[present, 0], start[present]) and torch.equal(rr[present, 1], (start + counts)[present])
+    assert bool((rr[~present] == 0).all())
+
+
+def test_inclusive_scan_beyond_2_pow_32_items():
+    """n = 2^32 + 4097 u32 values (a 64-bit count of items, sums wrapping mod 2^32): out[0] == x[0] and
+    out[i] - out[i-1] == x[i] (mod 2^32) for every i, which determines the inclusive scan completely."""
+    n = (1 << 32) + 4097
+    gen = torch.Generator(device="cuda").manual_seed(32)
+    x = torch.randint(0, 1 << 20, (n,), device="cuda", generator=gen, dtype=torch.int32)
+    out = primitives.inclusive_scan_u32(x)
+    assert int(out[0]) == int(x[0])
+    d = out[1:] - out[:-1]  # int32 arithmetic wraps mod 2^32
+    assert torch.equal(d, x[1:])
+
+
 @pytest.mark.parametrize("case", ["d2_0.5_0.02", "one_tile_4m"])
 def test_queue_hand_offs_under_concurrent_load(case):
     """The partition queue's hand-offs (tags, countdowns, group countdowns) under UNEVEN load: the same
