@@ -10,7 +10,9 @@
 // initialised to FLT_MAX (so P <= 3 yields FLT_MAX / inf terms exactly as there,
 // simple_knn.cu:155), a point never matches itself by index (duplicates count as
 // distance 0, :159,178), result ((b0 + b1) + b2) / 3.0f (:183).  The squared distance
-// is evaluated as fmaf(dz,dz, fmaf(dy,dy, dx*dx)) on device and in the oracle.
+// d.x*d.x + d.y*d.y + d.z*d.z (:136) is evaluated as fmaf(dz,dz, fmaf(dx,dx, dy*dy)) on device and
+// in the oracle: the contraction an LLVM-based CUDA compiler gives that expression (the left product
+// of `a*b + c*d` fused; DESIGN.md "Parity").
 //
 // Search (MI355X-first):
 //   1. bounding box (grid-stride partial min/max + one finishing workgroup) -- no host
@@ -72,7 +74,7 @@ inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 __device__ __forceinline__ float sqdist(float4 q, float4 c)
 {
     const float dx = c.x - q.x, dy = c.y - q.y, dz = c.z - q.z;
-    return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+    return fmaf(dz, dz, fmaf(dx, dx, dy * dy));
 }
 
 // Lower bound of sqdist(q, c) over c in the box, same monotone expression as sqdist.
@@ -81,7 +83,7 @@ __device__ __forceinline__ float box_point_lb(const Box& b, float4 q)
     const float gx = fmaxf(fmaxf(b.lo.x - q.x, q.x - b.hi.x), 0.f);
     const float gy = fmaxf(fmaxf(b.lo.y - q.y, q.y - b.hi.y), 0.f);
     const float gz = fmaxf(fmaxf(b.lo.z - q.z, q.z - b.hi.z), 0.f);
-    return fmaf(gz, gz, fmaf(gy, gy, gx * gx));
+    return fmaf(gz, gz, fmaf(gx, gx, gy * gy));
 }
 
 // Lower bound over every query in the AABB [qlo, qhi] and every point of the box.
@@ -90,7 +92,7 @@ __device__ __forceinline__ float box_box_lb(const Box& b, float4 qlo, float4 qhi
     const float gx = fmaxf(fmaxf(b.lo.x - qhi.x, qlo.x - b.hi.x), 0.f);
     const float gy = fmaxf(fmaxf(b.lo.y - qhi.y, qlo.y - b.hi.y), 0.f);
     const float gz = fmaxf(fmaxf(b.lo.z - qhi.z, qlo.z - b.hi.z), 0.f);
-    return fmaf(gz, gz, fmaf(gy, gy, gx * gx));
+    return fmaf(gz, gz, fmaf(gx, gx, gy * gy));
 }
 
 // Keep the three smallest values seen (a multiset, as updateKBest<3> does).  NaN never enters.

@@ -105,7 +105,7 @@ int hidegs_mark_visible(int P, const float* means3D, const float* viewmatrix, co
 /*
  * distCUDA2: for each of P points (P,3) fp32, the mean of the squared distances to its
  * 3 nearest other points, written to mean_dists (P).  Exact 3-NN:
- * squared distance fmaf(dz,dz,fmaf(dy,dy,dx*dx)) of (candidate - query), three best
+ * squared distance fmaf(dz,dz,fmaf(dx,dx,dy*dy)) of (candidate - query), three best
  * initialised to FLT_MAX (P <= 3 keeps FLT_MAX terms: P = 1, 2 give inf, P = 3 gives
  * FLT_MAX/3), a point never matches itself (duplicates give 0), result
  * ((b0 + b1) + b2) / 3.0f.  scratch_buffer receives exactly one request of

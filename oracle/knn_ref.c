@@ -10,10 +10,11 @@
  *   - for each query i, the three smallest squared distances to points j != i (by index,
  *     so duplicates contribute 0; simple_knn.cu:159,178), kept as updateKBest<3> keeps them
  *     (strict '>' insertion into a list initialised to FLT_MAX, :133-146,155);
- *   - squared distance of d = candidate - query (:135-136), evaluated here and on the
- *     device as fmaf(dz, dz, fmaf(dy, dy, dx * dx)) -- the rounding is pinned so that
- *     device and oracle agree bit for bit (the reference's own contraction under nvcc
- *     cannot be observed here; see DESIGN.md, "Parity");
+ *   - squared distance of d = candidate - query (:135-136), d.x*d.x + d.y*d.y + d.z*d.z,
+ *     evaluated here and on the device as fmaf(dz, dz, fmaf(dx, dx, dy * dy)): the
+ *     contraction clang and gcc give that very expression under FMA contraction (the left
+ *     product of a*b + c*d fused; tools/probe_contraction.c), which an LLVM-based nvcc shares
+ *     (nvcc itself cannot run here; see DESIGN.md, "Parity");
  *   - result ((b0 + b1) + b2) / 3.0f (:183).
  * The reference's search (Morton boxes, :186-221) is exact, so it returns this value.
  * Brute force, O(P^2): used at P <= ~1e5 and on sampled queries at larger P.
@@ -28,7 +29,7 @@
 static inline float sqdist(const float* q, const float* c)
 {
     const float dx = c[0] - q[0], dy = c[1] - q[1], dz = c[2] - q[2];
-    return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+    return fmaf(dz, dz, fmaf(dx, dx, dy * dy));
 }
 
 static inline void update_kbest3(float dist, float* knn)

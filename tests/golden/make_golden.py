@@ -22,12 +22,33 @@ import json
 import os
 import sys
 
+from fractions import Fraction
+
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 F32_MAX = np.float32(np.finfo(np.float32).max)
+
+
+def f32_round(x: Fraction) -> np.float32:
+    """x rounded once to the nearest float32 (ties to even): what a fused multiply-add returns."""
+    c = np.float32(float(x))  # within one float32 ulp of x (float() itself rounds to float64 first)
+    best = None
+    for y in (np.nextafter(c, np.float32(-np.inf)), c, np.nextafter(c, np.float32(np.inf))):
+        if not np.isfinite(y):
+            continue
+        err = abs(Fraction(float(y)) - x)
+        key = (err, int(np.float32(y).view(np.uint32)) & 1)  # nearer first, then the even significand
+        if best is None or key < best[0]:
+            best = (key, y)
+    return np.float32(best[1])
+
+
+def fma32(a, b, c) -> np.float32:
+    """fmaf(a, b, c): the exact a*b + c rounded once."""
+    return f32_round(Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c)))
 
 
 def by_definition(pts):
@@ -41,10 +62,10 @@ def by_definition(pts):
                 if i == j:
                     continue
                 d = pts[j] - pts[i]
-                # fmaf(dz,dz,fmaf(dy,dy,dx*dx)): exact in float64 then rounded once per fma
-                a = np.float32(d[0] * d[0])
-                b = np.float32(np.float64(d[1]) * np.float64(d[1]) + np.float64(a))
-                dist = np.float32(np.float64(d[2]) * np.float64(d[2]) + np.float64(b))
+                # d.x*d.x + d.y*d.y + d.z*d.z contracted as fmaf(dz,dz,fmaf(dx,dx,dy*dy)),
+                # each fma exact then rounded once
+                a = np.float32(d[1] * d[1])
+                dist = fma32(d[2], d[2], fma32(d[0], d[0], a))
                 for k in range(3):
                     if best[k] > dist:
                         best[k], dist = dist, best[k]
