@@ -27,6 +27,8 @@
 #include "block_scan.h"
 #include "common.h"
 
+#include <mutex>
+
 namespace hidegs {
 int identify_tile_ranges(const uint64_t* keys, long long n, uint32_t* ranges, int num_tiles, hipStream_t stream);
 
@@ -2754,10 +2756,15 @@ __global__ void queue_error_take_kernel(int clear)
 
 int queue_error(hipStream_t stream, int clear, uint32_t* flags)
 {
+    // one reader at a time: g_queue_error_read is a single word per device
+    static std::mutex m;
+    std::lock_guard<std::mutex> lock(m);
     uint32_t v = 0;
     hipLaunchKernelGGL(queue_error_take_kernel, dim3(1), dim3(1), 0, stream, clear);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(stream) != hipSuccess ||
-        hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_queue_error_read), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(g_queue_error_read), sizeof(v), 0, hipMemcpyDeviceToHost, stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
         return fail(HIDEGS_E_HIP, "queue_error: readback failed");
     // the asynchronous copy of the same failures: reported here and taken with the clear
     if (clear) v |= take_async_bits();
