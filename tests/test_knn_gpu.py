@@ -97,6 +97,25 @@ def test_degenerate_sets_bit_exact(oracle_lib, maker):
     assert_bits_equal(knn(pts), oracle_lib.knn_mean3(pts), maker)
 
 
+@pytest.mark.parametrize("case", ["nan_coordinates", "inf_coordinates", "nan_and_inf"])
+def test_non_finite_points_bit_exact(oracle_lib, case):
+    """Non-finite coordinates (a diverged point): the reference keeps a candidate only if
+    `knn[j] > dist` (simple_knn.cu:139), which is false for NaN and for +inf, so such points never enter
+    anyone's three best, and a NaN point's own result is (FLT_MAX x 3) / 3 = inf.  The search's Morton
+    codes, boxes and bounds must not let a non-finite point hide a finite neighbour."""
+    g = np.random.default_rng(23)
+    pts = g.random((20000, 3), dtype=np.float32)
+    idx = g.choice(20000, 40, replace=False)
+    if case in ("nan_coordinates", "nan_and_inf"):
+        pts[idx[:10], g.integers(0, 3, 10)] = np.nan
+        pts[idx[10:15]] = np.nan
+    if case in ("inf_coordinates", "nan_and_inf"):
+        pts[idx[15:25], g.integers(0, 3, 10)] = np.inf
+        pts[idx[25:30], g.integers(0, 3, 5)] = -np.inf
+        pts[idx[30:32]] = np.inf
+    assert_bits_equal(knn(pts), oracle_lib.knn_mean3(pts), case)
+
+
 def test_frustum_100k_every_point(oracle_lib):
     pts = frustum_points(100_000)
     assert_bits_equal(knn(pts), oracle_lib.knn_mean3(pts), "frustum 100k")
