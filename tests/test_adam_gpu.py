@@ -88,6 +88,52 @@ def test_against_torch_op_sequence_and_oracle(n, wd):
         assert float(st["step"]) == 6.0
 
 
+def same_bits_or_both_nan(a, b):
+    """Bit-identical, except that NaN only has to be NaN on both sides (payloads are the hardware's)."""
+    a, b = a.detach().cpu().reshape(-1), b.detach().cpu().reshape(-1)
+    na, nb = torch.isnan(a), torch.isnan(b)
+    return torch.equal(na, nb) and torch.equal(a[~na].view(torch.int32), b[~nb].view(torch.int32))
+
+
+def test_non_finite_and_extreme_gradients():
+    """Gradients a diverging step produces -- NaN, +-inf, squares that overflow (1e20, 1e30), denormals
+    (1e-40), signed zeros -- through three steps: every element as OurAdam's torch ops leave it on this
+    GPU (NaN positions equal, other bits equal), and as the C oracle leaves it."""
+    n = 5003
+    init = make(n, 17)
+    g = torch.Generator().manual_seed(18)
+    ours = {k: torch.nn.Parameter(v.clone().cuda()) for k, v in init.items()}
+    opt = Adam([{"params": [ours[k]], "lr": LRS[k], "name": k} for k in SHAPES], lr=0.0, eps=1e-15)
+    ref = {k: v.clone().cuda() for k, v in init.items()}
+    ref_state = {k: {"step": torch.tensor(0.), "exp_avg": torch.zeros_like(v), "exp_avg_sq": torch.zeros_like(v)}
+                 for k, v in ref.items()}
+    orc = {k: v.clone().numpy() for k, v in init.items()}
+    orc_state = {k: (np.zeros_like(v), np.zeros_like(v)) for k, v in orc.items()}
+    specials = torch.tensor([float("nan"), float("inf"), -float("inf"), 1e20, -1e30, 1e-40, -1e-40, 0.0, -0.0, 3e38])
+    for step in range(1, 4):
+        rel = torch.rand(n, generator=g) < 0.7
+        grads = {}
+        for k, s in SHAPES.items():
+            t = torch.randn((n, *s), generator=g)
+            pick = torch.rand(t.shape, generator=g) < 0.05
+            t[pick] = specials[torch.randint(0, specials.numel(), (int(pick.sum()),), generator=g)]
+            grads[k] = t
+            ours[k].grad = t.cuda()
+        opt.step(rel.cuda())
+        torch_reference_step(ref, {k: v.cuda() for k, v in grads.items()}, ref_state, rel.cuda(), LRS)
+        for k in SHAPES:
+            m, v = orc_state[k]
+            oracle.masked_adam(orc[k], grads[k].numpy().copy(), m, v, rel.numpy(), LRS[k], 0.9, 0.999, 1e-15, 0.0, step)
+    torch.cuda.synchronize()
+    for k in SHAPES:
+        st = opt.state[ours[k]]
+        assert same_bits_or_both_nan(ours[k], ref[k]), k
+        assert same_bits_or_both_nan(st["exp_avg"], ref_state[k]["exp_avg"]), k
+        assert same_bits_or_both_nan(st["exp_avg_sq"], ref_state[k]["exp_avg_sq"]), k
+        assert same_bits_or_both_nan(ours[k], torch.from_numpy(orc[k])), k
+        assert bool(torch.isnan(ours[k]).any()) and bool(torch.isfinite(ours[k]).any())
+
+
 def test_index_relevant_equals_bool_mask():
     n = 5000
     init = make(n, 3)
