@@ -94,6 +94,25 @@ def _link(objs, lib: str, verbose: bool) -> str:
     return lib
 
 
+ABI_CLIENT_SRC = os.path.join(HERE, "..", "tests", "c_abi", "abi_client.cpp")
+ABI_CLIENT = os.path.join(HERE, "..", "tests", "c_abi", "abi_client")
+
+
+def build_abi_client(verbose: bool = False) -> str:
+    """tests/c_abi/abi_client: a C++ program calling the ABI with no Python (test infrastructure, run on the
+    GPU by tests/test_c_abi_gpu.py), linked against the in-tree library with an $ORIGIN-relative rpath."""
+    deps = [ABI_CLIENT_SRC, LIB, os.path.join(INCLUDE, "hidegs.h")]
+    if not os.path.exists(ABI_CLIENT) or any(os.path.getmtime(d) > os.path.getmtime(ABI_CLIENT) for d in deps):
+        tmp = ABI_CLIENT + ".tmp"
+        cmd = [hipcc(), "--offload-arch=gfx950", "-O2", "-std=c++17", "-ffp-contract=off", "-Wall", ABI_CLIENT_SRC,
+               "-L" + HERE, "-lhidegs", "-Wl,-rpath,$ORIGIN/../../hidegs_amd", "-o", tmp]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, ABI_CLIENT)
+    return ABI_CLIENT
+
+
 def variant_path(tag: str) -> str:
     return os.path.join(VARIANT_DIR, f"libhidegs_{tag}.so")
 
@@ -117,6 +136,7 @@ def build(verbose: bool = False, variants: bool = True) -> str:
             own = dict(zip(changed, objs[k:k + len(changed)]))
             k += len(changed)
             _link([own.get(s, o) for s, o in zip(SOURCES, base)], variant_path(tag), verbose)
+        build_abi_client(verbose)
     return LIB
 
 
