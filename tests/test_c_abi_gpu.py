@@ -11,8 +11,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLIENT = os.path.join(ROOT, "tests", "c_abi", "abi_client")
 
 
-def test_client_is_built_against_the_in_tree_library():
-    assert os.path.exists(CLIENT), "run python -m hidegs_amd.build"
+def test_client_is_built_against_the_in_tree_library(built_lib):
+    assert os.path.exists(CLIENT), "python -m hidegs_amd.build builds it"
     out = subprocess.run(["readelf", "-d", CLIENT], capture_output=True, text=True).stdout
     assert "libhidegs.so" in out and "$ORIGIN/../../hidegs_amd" in out
 
