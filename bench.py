@@ -28,8 +28,9 @@ on this path is measured for real, at the configuration the metric is quoted on 
               a small disc: ~70 tiles over 8192 pairs take the partition queue).
   distCUDA2 = simple_knn._C.distCUDA2 on the 2M D2 centres, with its issue-rate roofline (VALU
               wave-instructions per second from the committed PMC summary, against the chip's).
-  config5_scale = the binning step and distCUDA2 at config 5's size (10M Gaussians, 4K frame).
-              binning_skewed and config5_scale are single-GPU sub-metrics: measured at N = 1 only.
+  config2_scale / config5_scale = the binning step and distCUDA2 at config 2's size (100k Gaussians,
+              1080p) and config 5's (10M Gaussians, 4K frame).  binning_skewed and the config scales
+              are single-GPU sub-metrics: measured at N = 1 only.
   exchange  = the view-DP exchange of 2M x 59 fp32 leaf gradients + stats over RCCL (no
               collective at N = 1), HIP-event timed; algbw and ring busbw.  exchange_bf16: the same
               with the bf16 wire (all-to-all + fp32 sums + all-gather; view_dp.py, transport="bf16").
@@ -189,7 +190,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exchange", action="store_true")
     ap.add_argument("--no-adam", action="store_true")
-    ap.add_argument("--no-config5", action="store_true")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config 2 and config 5 scale sub-metrics")
     ap.add_argument("--no-skewed", action="store_true")
     return ap.parse_args()
 
@@ -440,6 +441,18 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
                                     "achieved_wave_instr_per_s": rate, "peak_wave_instr_per_s": VALU_PEAK_WAVE_INSTR_PER_S,
                                     "frac": round(rate / VALU_PEAK_WAVE_INSTR_PER_S, 4), "pmc_source": KNN_PMC_FILE[len(ROOT) + 1:]}
     line["distCUDA2"] = kd
+
+    # ---- config 2's scale: 100k Gaussians, 1920x1080 ------------------------------------------------
+    if not args.no_config5 and world == 1:  # single-GPU sub-metric, like config 5's below
+        sc2 = synthetic.d2_scene(100_000, cam, seed=rank)
+        wl2 = synthetic.d2_binning_workload(sc2, cam, device=dev)
+        ms2, _ = timed(make_step(wl2), 50, 5)
+        pts2 = sc2.means3D.to(dev)
+        knn2_ms, _ = timed(lambda: simple_knn._C.distCUDA2(pts2), 10, 2)
+        line["config2_scale"] = {"workload": "100k D2 Gaussians, 1920x1080 (8160 tiles): binning step and distCUDA2",
+                                 "binning_ms_per_step": round(ms2, 4), "pairs_K": wl2.num_pairs,
+                                 "distCUDA2_ms": round(knn2_ms, 3), "queue_error": primitives.queue_error()}
+        del sc2, wl2, pts2
 
     # ---- config 5's scale: 10M Gaussians, 3840x2160 frame ----------------------------------------
     if not args.no_config5 and world == 1:  # single-GPU sub-metric (a 10M scene per rank is CPU time)
