@@ -2550,6 +2550,12 @@ constexpr long long kSegmentedMinN = 65536;  // below this the plain LSD passes 
 constexpr long long kSegmentedMinAvg = 64;   // pairs per segment on average, else the plain passes: one
                                              // workgroup per ~30-pair segment (distCUDA2's 48-bit Morton
                                              // keys of 2M points) costs more than the 4 low-digit passes
+#ifndef HIDEGS_TILE_SEG_MIN_AVG
+#define HIDEGS_TILE_SEG_MIN_AVG 8  // the same for hidegs_sort_tile_pairs, per tile of the caller's grid: small
+                                   // views (config 2, 100k Gaussians) took 6 plain passes, 105-115 us, against
+                                   // 68-70 us segmented (64 / 32 / 16 / 8 / 1 A/B in DESIGN.md, "Small views")
+#endif
+constexpr long long kTileSegmentedMinAvg = HIDEGS_TILE_SEG_MIN_AVG;
 
 // Capacities of the partition queue for n pairs.  Every record holds > kSegCap pairs and the
 // records of one level are disjoint: <= n / 2049 per level, 5 levels (4 digits + the copy).  A
@@ -2633,8 +2639,11 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
     uint32_t* totals_pass[2] = {c.take<uint32_t>(kRadix), c.take<uint32_t>(kRadix)};  // alternate passes
 
     // (tile | depth)-shaped sort: LSD over the segment bits only, then per-segment LDS sorts
+    // average pairs per segment: per tile of the caller's grid with ranges_out, else per segment-bit value
+    const bool avg_ok = ranges_out ? n >= kTileSegmentedMinAvg * (long long)num_tiles
+                                   : n >= (kSegmentedMinAvg << (end_bit - 32));
     const bool segmented = sizeof(K) == 8 && begin_bit == 0 && end_bit > 32 && end_bit - 32 <= kMaxSegmentBits &&
-                           n >= kSegmentedMinN && n >= (kSegmentedMinAvg << (end_bit - 32));
+                           n >= kSegmentedMinN && avg_ok;
     const int lo_bit = segmented ? 32 : begin_bit;
     const int lsd_passes = segmented ? (end_bit - 32 + kRadixBits - 1) / kRadixBits : passes;
 
