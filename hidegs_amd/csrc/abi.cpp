@@ -35,12 +35,19 @@ static int not_built(const char* fn) { return fail(HIDEGS_E_UNSUPPORTED, std::st
 
 namespace {
 std::once_flag g_async_once;
-uint32_t* g_async_host = nullptr;    // mapped, coherent pinned word
-uint32_t* g_async_device = nullptr;  // its device address
+std::atomic<uint32_t*> g_async_host{nullptr};    // mapped, coherent pinned word
+std::atomic<uint32_t*> g_async_device{nullptr};  // its device address (published after the host word)
 }  // namespace
 
-uint32_t* async_error_slot()
+uint32_t* async_error_slot(hipStream_t stream)
 {
+    // not allocated yet and the stream is being captured into a graph: no pinned allocation inside a
+    // capture (it may synchronise); that call goes without the asynchronous word
+    if (!g_async_device.load(std::memory_order_acquire)) {
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(stream, &st) != hipSuccess) (void)hipGetLastError();
+        if (st != hipStreamCaptureStatusNone) return nullptr;
+    }
     std::call_once(g_async_once, [] {
         void* h = nullptr;
         if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess) {
@@ -53,17 +60,18 @@ uint32_t* async_error_slot()
             (void)hipHostFree(h);
             return;
         }
-        g_async_host = static_cast<uint32_t*>(h);
-        __atomic_store_n(g_async_host, 0u, __ATOMIC_SEQ_CST);
-        g_async_device = static_cast<uint32_t*>(d);
+        __atomic_store_n(static_cast<uint32_t*>(h), 0u, __ATOMIC_SEQ_CST);
+        g_async_host.store(static_cast<uint32_t*>(h), std::memory_order_release);
+        g_async_device.store(static_cast<uint32_t*>(d), std::memory_order_release);
     });
-    return g_async_device;
+    return g_async_device.load(std::memory_order_acquire);
 }
 
 uint32_t take_async_bits()
 {
     // the word exists only once a sort asked for its slot; before that nothing can be pending
-    return g_async_host ? __atomic_exchange_n(g_async_host, 0u, __ATOMIC_SEQ_CST) : 0u;
+    uint32_t* h = g_async_host.load(std::memory_order_acquire);
+    return h ? __atomic_exchange_n(h, 0u, __ATOMIC_SEQ_CST) : 0u;
 }
 
 int take_async_error(const char* what)

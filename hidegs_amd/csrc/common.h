@@ -39,8 +39,9 @@ int queue_error(hipStream_t stream, int clear, uint32_t* flags);
 // Asynchronous error word: one u32 of mapped, coherent pinned host memory that a sort's last kernel
 // sets (system-scope store) when its partition queue failed, so that the failure surfaces without a
 // host synchronisation.  async_error_slot() returns its device address (NULL if it could not be
-// allocated: then only the debug mode and hidegs_queue_error report queue errors).
-uint32_t* async_error_slot();
+// allocated, or the first request comes from a stream being captured into a graph: then only the debug
+// mode and hidegs_queue_error report that call's queue errors).
+uint32_t* async_error_slot(hipStream_t stream);
 // Called first by every compute entry point: a set word is taken (exchanged with 0) and turned into
 // HIDEGS_E_ASYNC with its message, so the call after a failed sort fails loudly instead of running.
 int take_async_error(const char* what);

@@ -2727,7 +2727,7 @@ int sort_pairs(void* scratch, size_t scratch_bytes, const K* keys_in, K* keys_ou
         // debug mode checks this call's queue itself (below); otherwise the last kernel hands a queue
         // error to the mapped host word, which fails the next entry-point call
         const bool debug = debug_enabled();
-        uint32_t* async_err = debug ? nullptr : async_error_slot();
+        uint32_t* async_err = debug ? nullptr : async_error_slot(stream);
         static_assert(kDeferPieces, "piece_sort_kernel is the sort's last kernel: it reports the queue's error");
         HIDEGS_LAUNCH("piece_sort", piece_sort_kernel, dim3(kPieceBlocks), dim3(kBlock), 0, stream, ko, vals_out,
                       reinterpret_cast<const uint64_t*>(alt_k), alt_v, q, async_err);

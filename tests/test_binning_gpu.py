@@ -1,5 +1,7 @@
 """Binning primitives on the MI355X (hidegs_amd/csrc/primitives.hip) against generic integer
 oracles (oracle/binning.py).  Integer work: every result must be bit-identical."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -662,6 +664,40 @@ def test_sort_tile_pairs_at_the_maximum_size():
     present = counts > 0
     assert torch.equal(rr[present, 0], start[present]) and torch.equal(rr[present, 1], (start + counts)[present])
     assert bool((rr[~present] == 0).all())
+
+
+def test_binning_step_captured_in_a_graph_as_the_first_sort():
+    """The binning step (scan + sort_tile_pairs) captured into a hipGraph (torch.cuda.CUDAGraph) before the
+    process has sorted anything: the first sort must not allocate the asynchronous error word inside the
+    capture (async_error_slot skips it then), and replays give the stable sort's result.  A fresh process,
+    so the capture really is the first sort."""
+    import subprocess
+    import sys
+    code = r"""
+import sys, torch
+sys.path.insert(0, %r)
+from hidegs_amd import primitives, synthetic
+wl = synthetic.binning_workload(300_000, 1920, 1080, seed=9, device="cuda")
+off = torch.empty_like(wl.tiles_touched)
+torch.cuda.synchronize()
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    primitives.inclusive_scan_u32(wl.tiles_touched, out=off)
+    ko, vo, r = primitives.sort_tile_pairs(wl.keys, wl.values, wl.num_tiles)
+for _ in range(3):
+    ko.zero_(); vo.zero_()
+    g.replay()
+torch.cuda.synchronize()
+end = 32 + primitives.higher_msb(wl.num_tiles)
+ek, perm = torch.sort(wl.keys & ((1 << end) - 1), stable=True)
+assert torch.equal(vo, wl.values[perm]) and torch.equal(ko, wl.keys[perm]), "graph replay differs"
+assert torch.equal(off, torch.cumsum(wl.tiles_touched, 0, dtype=torch.int32))
+ko2, vo2, r2 = primitives.sort_tile_pairs(wl.keys, wl.values, wl.num_tiles)  # eager afterwards
+assert torch.equal(vo2, vo) and torch.equal(r2, r) and primitives.queue_error() == 0
+print("GRAPH_OK", wl.num_pairs)
+""" % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0 and "GRAPH_OK" in out.stdout, out.stdout[-2000:] + out.stderr[-3000:]
 
 
 def test_inclusive_scan_beyond_2_pow_32_items():
