@@ -42,3 +42,20 @@ for _ in range(50):
     torch.cuda.synchronize()
     ts.append(e0.elapsed_time(e1) * 1e3 / 10)
 print(f"back to back: {statistics.median(ts):.1f} us per step", flush=True)
+
+# the same step captured once into a hipGraph and replayed (launch latency off the critical path)
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    step()
+for _ in range(10):
+    g.replay()
+ts = []
+for _ in range(50):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    ts.append(e0.elapsed_time(e1) * 1e3 / 10)
+print(f"graph replay, back to back: {statistics.median(ts):.1f} us per step", flush=True)
