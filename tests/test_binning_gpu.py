@@ -746,6 +746,55 @@ def test_queue_hand_offs_under_concurrent_load(case):
         assert primitives.queue_error() == 0
 
 
+def test_concurrent_sorts_from_host_threads_on_their_own_streams():
+    """B5 "re-entrant per device": four host threads, each on its own stream, sort different views at the
+    same time (hot tiles included, so up to four partition queues run concurrently), four times each.
+    Every result equals torch's stable sort of the same keys; no queue error, no asynchronous error."""
+    import threading
+
+    from hidegs_amd import synthetic
+    cam = synthetic.d2_camera(1920, 1080)
+    cases = []
+    for seed, cluster in ((2001, (0.5, 0.02)), (2002, (0.15, 0.1)), (2003, None)):
+        wl = synthetic.d2_binning_workload(synthetic.d2_scene(1_000_000, cam, seed=seed, cluster=cluster), cam,
+                                           device="cuda")
+        cases.append((wl.keys, wl.values, wl.num_tiles))
+    g = torch.Generator(device="cuda").manual_seed(12)
+    n = 1_500_000
+    depth = torch.empty(n, device="cuda").uniform_(0.2, 100.0, generator=g)
+    one = (torch.full((n,), 77, dtype=torch.int64, device="cuda") << 32) | depth.view(torch.int32).to(torch.int64)
+    cases.append((one, torch.arange(n, dtype=torch.int32, device="cuda"), 8160))
+    expected = []
+    for keys, vals, _ in cases:
+        _, perm = torch.sort(keys, stable=True)
+        expected.append((keys[perm], vals[perm]))
+    torch.cuda.synchronize()
+    failures = []
+
+    def worker(i):
+        try:
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.default_stream())
+            keys, vals, T = cases[i]
+            with torch.cuda.stream(st):
+                for rep in range(4):
+                    ko, vo, _ = primitives.sort_tile_pairs(keys, vals, T)
+                    st.synchronize()
+                    if not (torch.equal(ko, expected[i][0]) and torch.equal(vo, expected[i][1])):
+                        failures.append(f"case {i} repetition {rep}")
+        except Exception as e:  # noqa: BLE001 -- reported below
+            failures.append(f"case {i}: {e!r}")
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(len(cases))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(120)
+    assert not any(t.is_alive() for t in threads), "a sorting thread did not finish"
+    assert not failures, failures
+    assert primitives.queue_error() == 0
+
+
 def test_pieces_beyond_a_full_piece_list_variant():
     """The queue's pieces go to piece_sort_kernel's list; a build whose list holds 16 (build.VARIANTS['pcap'])
     runs every later piece as a SMALL queue job -- the same result, bit for bit, on a D2 view with hot
