@@ -116,6 +116,38 @@ def test_non_finite_points_bit_exact(oracle_lib, case):
     assert_bits_equal(knn(pts), oracle_lib.knn_mean3(pts), case)
 
 
+def test_concurrent_calls_from_host_threads(oracle_lib):
+    """Three host threads, each on its own stream, run distCUDA2 on different clouds at once (its scratch
+    callback, sort and search interleave on the device); every result bit-identical to the oracle."""
+    import threading
+    clouds = [frustum_points(30000, seed=s) for s in (31, 32)] + [sfm_like(30000, seed=33)]
+    expected = [oracle_lib.knn_mean3(c) for c in clouds]
+    dev = [torch.from_numpy(np.ascontiguousarray(c)).cuda() for c in clouds]
+    torch.cuda.synchronize()
+    got, failures = [None] * 3, []
+
+    def worker(i):
+        try:
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.default_stream())
+            with torch.cuda.stream(st):
+                for _ in range(3):
+                    out = simple_knn._C.distCUDA2(dev[i])
+                st.synchronize()
+                got[i] = out.cpu().numpy()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            failures.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(3)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(120)
+    assert not failures, failures
+    for i in range(3):
+        assert_bits_equal(got[i], expected[i], f"thread {i}")
+
+
 def test_frustum_100k_every_point(oracle_lib):
     pts = frustum_points(100_000)
     assert_bits_equal(knn(pts), oracle_lib.knn_mean3(pts), "frustum 100k")
