@@ -116,6 +116,6 @@ int hidegs_mark_visible(int, const float*, const float*, const float*, unsigned 
 void hidegs_set_debug(int enable) { hidegs::g_debug.store(enable ? 1 : 0, std::memory_order_relaxed); }
 
 const char* hidegs_last_error(void) { return hidegs::last_error().c_str(); }
-const char* hidegs_version(void) { return "hidegs-abi 0.5 (gfx950: distCUDA2, scan, radix sort, tile sort + ranges, masked Adam, view-DP wire)"; }
+const char* hidegs_version(void) { return "hidegs-abi 0.6 (gfx950: distCUDA2, scan, radix sort, tile sort + ranges, masked Adam, view-DP wire; HIDEGS_E_ASYNC)"; }
 
 }  // extern "C"
