@@ -18,6 +18,11 @@ P = os.path.join(ROOT, "profiles")
 
 def main():
     name, title, note = sys.argv[1:4]
+    need = [os.path.join(G, "prof_kt", "kt_kernel_stats.csv"), os.path.join(G, "prof_fetch"), os.path.join(G, "prof_write"),
+            os.path.join(G, "bench.json"), os.path.join(G, "gputest.log")]
+    missing = [p for p in need if not os.path.exists(p)]
+    if missing:  # a failed or partial session: change nothing under profiles/
+        sys.exit(f"profile_note: missing {missing}")
     kj = os.path.join(P, f"{name}_kernels.json")
     table = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof_summary.py"), os.path.join(G, "prof_kt"),
                             os.path.join(G, "prof_fetch"), os.path.join(G, "prof_write")], check=True, capture_output=True,
