@@ -36,7 +36,12 @@ on this path is measured for real, at the configuration the metric is quoted on 
               with the bf16 wire (all-to-all + fp32 sums + all-gather; view_dp.py, transport="bf16").
   exchange_and_step = the exchange followed by the masked step, sequential and overlapped.
   dp_step   = the rank's binning step + exchange_and_step, per wire format: the built part of one
-              view-DP training step (views/s over all ranks; no rasterizer), for the scaling runs.
+              view-DP training step (steps/s over all ranks; no rasterizer), for the scaling runs.  At
+              N = 1 the group issues no collective, so it is binning + masked Adam only (the keys say so:
+              binning_adam_steps_per_s); every exchange sub-line carries its collective count and
+              "rasterizer": false.
+  fail fast = init_process_group(timeout=--pg-timeout): RCCL's watchdog ends a rank whose collective
+              never completes; gloo exchange waits are bounded on the host (view_dp.py).
   masked Adam = the fused row-masked optimizer step at 2M Gaussians (59 fp32 each), 90% visible.
   cpu_baseline = on rank 0 at N = 1, every CPU leg on the same `cores` threads (cpu_share(): the
               CPUs the process may run on, lowered to a cgroup quota, else to the harness's declared
@@ -47,8 +52,10 @@ Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
+import math
 import platform
 import socket
 import subprocess
@@ -192,6 +199,9 @@ def parse():
     ap.add_argument("--no-adam", action="store_true")
     ap.add_argument("--no-config5", action="store_true", help="skip the config 2 and config 5 scale sub-metrics")
     ap.add_argument("--no-skewed", action="store_true")
+    ap.add_argument("--pg-timeout", type=float, default=120.0,
+                    help="seconds: the process group's timeout (RCCL watchdog: a collective that never completes "
+                         "ends the process) and the exchange's bounded host waits (gloo)")
     return ap.parse_args()
 
 
@@ -242,7 +252,10 @@ def main() -> None:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ["MASTER_PORT"] = str(free_port())
         kw = {"device_id": dev} if gpu else {}
-        dist.init_process_group(args.backend, rank=rank, world_size=world, **kw)
+        # fail fast: a rank that stalls or dies ends the run within the timeout instead of hanging
+        # it -- RCCL's watchdog aborts a collective older than this; gloo operations time out after it
+        dist.init_process_group(args.backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=args.pg_timeout), **kw)
 
     from hidegs_amd import synthetic
     from hidegs_amd.view_dp import GradArena, ViewDPExchange
@@ -297,6 +310,10 @@ def main() -> None:
                   "(DESIGN.md, 'Decisions in force'); value stays null",
         "roofline": None,
         "cpu_baseline": None,
+        "fail_fast": {"process_group_timeout_s": args.pg_timeout, "exchange_host_wait_timeout_s": args.pg_timeout,
+                      "rccl": "watchdog aborts a collective older than the process group timeout and ends the "
+                              "process; the exchange's waits are stream waits (no host block)",
+                      "gloo": "every exchange wait bounded on the host, RuntimeError naming the collective"},
     }
     cam = synthetic.d2_camera(W_PX, H_PX)
     scene = synthetic.d2_scene(N, cam, seed=rank)
@@ -385,8 +402,10 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
             meta = json.load(f)
     sort_us = sum(kern[k]["us_per_step"] for k in kern if k in SORT_KERNELS)
     line["binning_step"] = {"ms_per_step": round(ms_step, 4), "wall_ms_per_step": round(wall_ms_step, 4),
+                            "timed_region": "inclusive scan of tiles_touched + hidegs_sort_tile_pairs (sort + "
+                                            "tile ranges); no key emission, no rasterizer",
                             "pairs_per_s_all_ranks": K * world / (ms_step * 1e-3),
-                            "views_per_s_all_ranks": world / (ms_step * 1e-3),
+                            "binning_steps_per_s_all_ranks": world / (ms_step * 1e-3),
                             "sort_us": round(sort_us, 2), "queue_error": qerr, "kernels": kern}
     line["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
@@ -490,16 +509,24 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
             torch.cuda.synchronize()
             k_ms, k_n = kt.get("masked_adam")
         st = {k: (torch.zeros_like(p), torch.zeros_like(p)) for k, p in prm.items()}
+        ref_t = [0]
 
-        def ref_step():  # the reference's op sequence on the same GPU (OurAdam.py:249-337)
+        def ref_step():
+            """OurAdam's masked, non-capturable path as torch ops on the same GPU (scene/OurAdam.py:266-337):
+            gather the relevant rows, the two moment updates, bias_correction1/2 from the step count (host
+            floats, as step_t.item()), denom = sqrt(v) / bias_correction2_sqrt + eps, addcdiv_ with
+            -lr / bias_correction1, scatter the rows back."""
+            ref_t[0] += 1
+            bc1, bc2 = 1 - 0.9 ** ref_t[0], 1 - 0.999 ** ref_t[0]
+            bc2_sqrt = math.sqrt(bc2)
             with torch.no_grad():
                 for k, parami in prm.items():
                     m_all, v_all = st[k]
                     grad, exp_avg, exp_avg_sq, param = parami.grad[vis], m_all[vis], v_all[vis], parami[vis]
                     exp_avg.mul_(0.9).add_(grad, alpha=1 - 0.9)
-                    exp_avg_sq.mul_(0.999).addcmul_(grad, grad, value=1 - 0.999)
-                    denom = (exp_avg_sq.sqrt() / 0.5).add_(1e-15)
-                    param.addcdiv_(exp_avg, denom, value=-lrs[k])
+                    exp_avg_sq.mul_(0.999).addcmul_(grad, grad.conj(), value=1 - 0.999)
+                    denom = (exp_avg_sq.sqrt() / bc2_sqrt).add_(1e-15)
+                    param.addcdiv_(exp_avg, denom, value=-(lrs[k] / bc1))
                     m_all[vis] = exp_avg
                     v_all[vis] = exp_avg_sq
                     parami[vis] = param
@@ -509,6 +536,8 @@ def _gpu_legs(args, line, ctx, world, rank, dev, cam, scene, timed, np, torch):
                                "algorithmic_bytes": ad_bytes, "GBps": round(ad_bytes / (ad_ms * 1e-3) / 1e9, 1),
                                "hbm_frac": round(ad_bytes / (ad_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                                "reference_torch_ops_ms": round(ref_ms, 3),
+                               "reference_torch_ops": "scene/OurAdam.py:266-337 masked path as torch ops on this "
+                                                      "GPU, bias-corrected step_size and bias_correction2_sqrt",
                                "speedup_vs_reference_ops": round(ref_ms / ad_ms, 2)}
         ctx["adam_state"] = (prm, opt, vis, g)
     ctx["binning_pairs"] = (wl, end_bit, sort_us)
@@ -537,7 +566,7 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
         return all(torch.equal(x, got[0]) for x in got)
 
     for transport in ("fp32", "bf16"):
-        ex = ViewDPExchange(transport=transport)
+        ex = ViewDPExchange(transport=transport, timeout=args.pg_timeout)
         same = replicas_identical(ex)
         ex_ms, ex_wall = timed(lambda: ex.exchange(arena, visible, max_stats=[norm, radii]), reps, 2)
         nbytes = ex.last.reduced_bytes
@@ -551,11 +580,14 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
             "algbw_GBps": algbw,  # fp32 gradient bytes made consistent per second
             "busbw_GBps": None if algbw is None else algbw * 2 * (world - 1) / world,
             "collectives_per_step": ex.last.collectives, "compacted": ex.last.compacted,
-            "union_rows": ex.last.union_rows, "replicas_bit_identical": same}
+            "union_rows": ex.last.union_rows, "replicas_bit_identical": same, "rasterizer": False,
+            "timed_region": ("one-rank group: no collective, the visibility union only (the sum over one rank is "
+                             "its input)" if ex.last.collectives == 0 else
+                             f"{ex.last.collectives} collectives: visibility all-gather, gradient buckets, MAX")}
         if world == 1 and gpu:
             # the N-rank path forced on the one-rank group: every collective the multi-GPU run issues,
             # real RCCL calls (over one rank a copy), so the machinery's own cost is on the record
-            exf = ViewDPExchange(transport=transport, force_collectives=True)
+            exf = ViewDPExchange(transport=transport, force_collectives=True, timeout=args.pg_timeout)
             f_ms, _ = timed(lambda: exf.exchange(arena, visible, max_stats=[norm, radii]), reps, 2)
             line["exchange" if transport == "fp32" else "exchange_bf16"]["forced_one_rank_rccl"] = {
                 "ms_per_step": round(f_ms, 3), "collectives_per_step": exf.last.collectives,
@@ -568,7 +600,7 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
         for k, p in prm.items():
             arena2[k].copy_(p.grad)
         arena2.attach(prm)
-        ex2 = ViewDPExchange()
+        ex2 = ViewDPExchange(timeout=args.pg_timeout)
         norm2 = torch.rand(N, 1, device=dev, generator=g2)
 
         def seq_step():
@@ -577,22 +609,31 @@ def _exchange_legs(args, line, ctx, world, rank, dev, N, timed, gpu, torch, Grad
 
         seq_ms, _ = timed(seq_step, 10, 2)
         fused_ms, _ = timed(lambda: ex2.exchange_and_step(arena2, vis, opt, prm, max_stats=[norm2]), 10, 2)
-        ex3 = ViewDPExchange(transport="bf16")
+        ex3 = ViewDPExchange(transport="bf16", timeout=args.pg_timeout)
         bf16_ms, _ = timed(lambda: ex3.exchange_and_step(arena2, vis, opt, prm, max_stats=[norm2]), 10, 2)
         line["exchange_and_step"] = {"world": world, "sequential_ms": round(seq_ms, 3),
                                      "overlapped_ms": round(fused_ms, 3), "overlapped_bf16_ms": round(bf16_ms, 3),
-                                     "collectives": ex2.last.collectives, "union_rows": ex2.last.union_rows}
+                                     "collectives": ex2.last.collectives, "union_rows": ex2.last.union_rows,
+                                     "rasterizer": False,
+                                     "timed_region": ("masked Adam step only (one-rank group: no collective)"
+                                                      if ex2.last.collectives == 0 else
+                                                      "view-DP exchange + masked Adam step")}
         bin_step = ctx.get("binning_step")
         if bin_step is not None:
             # what this build runs of one view-DP training step, the rasterizer aside: the rank's view's
             # binning, the exchange and the masked optimizer step (overlapped), per wire format
-            dp = {"world": world, "includes": "binning step + view-DP exchange + masked Adam (overlapped); "
-                                              "no rasterizer fwd/bwd (refused)"}
+            dp = {"world": world, "rasterizer": False,
+                  "includes": ("binning step + masked Adam; one-rank group: no collective, no rasterizer fwd/bwd "
+                               "(refused)") if world == 1 else
+                              "binning step + view-DP exchange + masked Adam (overlapped); no rasterizer fwd/bwd "
+                              "(refused)"}
             for tag, exn in (("fp32", ex2), ("bf16", ex3)):
                 ms, _ = timed(lambda: (bin_step(), exn.exchange_and_step(arena2, vis, opt, prm, max_stats=[norm2])),
                               10, 2)
                 dp[f"{tag}_ms_per_step"] = round(ms, 3)
-                dp[f"{tag}_views_per_s_all_ranks"] = round(world / (ms * 1e-3), 1)
+                dp[f"{tag}_collectives"] = exn.last.collectives
+                rate = "binning_adam_steps_per_s" if world == 1 else "binning_exchange_adam_steps_per_s_all_ranks"
+                dp[f"{tag}_{rate}"] = round(world / (ms * 1e-3), 1)
             line["dp_step"] = dp
 
 
@@ -625,6 +666,8 @@ def _cpu_baselines(line, ctx, N, cam, np):
         dq = time.perf_counter() - t0
         line["distCUDA2"]["cpu_baseline"] = {
             "value": nq / dq, "unit": "queries/s", "cores": threads, "kind": "port",
+            "algorithm": "brute force over all points (the definition the oracle pins), NOT the reference's box "
+                         "search (SK/simple_knn.cu:148-184): the GPU/CPU ratio is not like for like",
             "sample": f"{nq} of the {N} D2 queries, each brute-forced against all points (oracle/knn_ref.c, OpenMP)",
             "gpu_queries_per_s": line["distCUDA2"]["points_per_s_all_ranks"]}
         del cpu_pts

@@ -48,7 +48,7 @@ SIGNATURES = {
                                       P, P, P, P,                 # cov3D_precomp, viewmatrix, projmatrix, campos
                                       F, F, P, F,                 # tan_fovx, tan_fovy, radii, h_var_bwd
                                       P, P, P,                    # geom, binning, image buffers
-                                      P, P, P, P,                 # dL_dpix, dL_dout_all_map, dL_dplane, dL_dinvdepth
+                                      P, P, P, P,                 # dL_dpix, dL_dout_all_map, dL_dplane, dL_invdepths
                                       P, P, P, P, P,              # dL_dmean2D, opacity, color, mean3D, cov3D
                                       P, P, P, P,                 # dL_dsh, dL_dscale, dL_drot, dL_dall_map
                                       I, I, P]),                  # render_geo, debug, stream

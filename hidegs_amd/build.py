@@ -35,7 +35,8 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=o
 
 # tag -> (extra defines, the sources they change); the other objects are shared with the product build
 VARIANTS = {
-    "qcap": (["-DHIDEGS_JOB_CAP=64"], ["primitives.hip"]),  # partition-queue overflow -> error word
+    # partition-queue overflow -> error word; its starved workers give up after 2^16 polls (~0.2 s), not ~13 s
+    "qcap": (["-DHIDEGS_JOB_CAP=64", "-DHIDEGS_MAX_POLLS=65536u"], ["primitives.hip"]),
     "gform": (["-DHIDEGS_QUEUE_MIN=8192"], ["primitives.hip"]),  # tiles of 2049..8192 pairs: one-workgroup global form
     "wscout": (["-DHIDEGS_WIDE_SCOUTS=1"], ["primitives.hip"]),  # hot tiles <= 12288 pairs as WIDE jobs (in place)
     "pcap": (["-DHIDEGS_PIECE_CAP=16"], ["primitives.hip"]),  # piece list full after 16: the rest as SMALL jobs

@@ -8,6 +8,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <unordered_map>
 
 namespace hidegs {
 
@@ -34,23 +35,34 @@ int check_launch(const char* stage, hipStream_t stream, int debug)
 static int not_built(const char* fn) { return fail(HIDEGS_E_UNSUPPORTED, std::string(fn) + ": " + kNotBuilt); }
 
 namespace {
+// One word per stream (a process-wide word reported thread A's failed sort on thread B's
+// unrelated call and let a second failure overwrite the first's bits).  Streams past the table share
+// word 0.  A stream handle that is destroyed and handed out again keeps its word.
+constexpr int kAsyncWords = 1024;
 std::once_flag g_async_once;
-std::atomic<uint32_t*> g_async_host{nullptr};    // mapped, coherent pinned word
-std::atomic<uint32_t*> g_async_device{nullptr};  // its device address (published after the host word)
-}  // namespace
+std::atomic<uint32_t*> g_async_host{nullptr};    // mapped, coherent pinned page of kAsyncWords words
+std::atomic<uint32_t*> g_async_device{nullptr};  // its device address (published after the host page)
+std::mutex g_slot_mutex;
+std::unordered_map<hipStream_t, int> g_slot;  // stream -> word index, guarded by g_slot_mutex
+int g_next_slot = 1;
 
-uint32_t* async_error_slot(hipStream_t stream)
+bool capturing(hipStream_t stream)
 {
-    // not allocated yet and the stream is being captured into a graph: no pinned allocation inside a
-    // capture (it may synchronise); that call goes without the asynchronous word
-    if (!g_async_device.load(std::memory_order_acquire)) {
-        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(stream, &st) != hipSuccess) (void)hipGetLastError();
-        if (st != hipStreamCaptureStatusNone) return nullptr;
-    }
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess) (void)hipGetLastError();
+    return st != hipStreamCaptureStatusNone;
+}
+
+// The page, allocated by the first call from a stream that is not being captured (no pinned
+// allocation inside a capture: it may synchronise).  Every entry point asks first, so a sort captured
+// into a graph finds the page already there unless every earlier call was captured too.
+void ensure_async_page(hipStream_t stream)
+{
+    if (g_async_device.load(std::memory_order_acquire) || capturing(stream)) return;
     std::call_once(g_async_once, [] {
         void* h = nullptr;
-        if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess) {
+        const size_t bytes = kAsyncWords * sizeof(uint32_t);
+        if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess) {
             (void)hipGetLastError();
             return;
         }
@@ -60,26 +72,48 @@ uint32_t* async_error_slot(hipStream_t stream)
             (void)hipHostFree(h);
             return;
         }
-        __atomic_store_n(static_cast<uint32_t*>(h), 0u, __ATOMIC_SEQ_CST);
+        for (int i = 0; i < kAsyncWords; i++) __atomic_store_n(static_cast<uint32_t*>(h) + i, 0u, __ATOMIC_SEQ_CST);
         g_async_host.store(static_cast<uint32_t*>(h), std::memory_order_release);
         g_async_device.store(static_cast<uint32_t*>(d), std::memory_order_release);
     });
-    return g_async_device.load(std::memory_order_acquire);
 }
 
-uint32_t take_async_bits()
+// `stream`'s word index; -1 if it has none and `create` is false (no sort ever reported to it).
+int slot_of(hipStream_t stream, bool create)
 {
-    // the word exists only once a sort asked for its slot; before that nothing can be pending
+    std::lock_guard<std::mutex> lock(g_slot_mutex);
+    auto it = g_slot.find(stream);
+    if (it != g_slot.end()) return it->second;
+    if (!create) return -1;
+    const int s = g_next_slot < kAsyncWords ? g_next_slot++ : 0;
+    g_slot.emplace(stream, s);
+    return s;
+}
+}  // namespace
+
+uint32_t* async_error_slot(hipStream_t stream)
+{
+    ensure_async_page(stream);
+    uint32_t* d = g_async_device.load(std::memory_order_acquire);
+    return d ? d + slot_of(stream, true) : nullptr;
+}
+
+uint32_t take_async_bits(hipStream_t stream)
+{
     uint32_t* h = g_async_host.load(std::memory_order_acquire);
-    return h ? __atomic_exchange_n(h, 0u, __ATOMIC_SEQ_CST) : 0u;
+    if (!h) return 0u;
+    const int s = slot_of(stream, false);
+    return s < 0 ? 0u : __atomic_exchange_n(h + s, 0u, __ATOMIC_SEQ_CST);
 }
 
-int take_async_error(const char* what)
+int take_async_error(const char* what, hipStream_t stream)
 {
-    const uint32_t err = take_async_bits();
+    ensure_async_page(stream);
+    const uint32_t err = take_async_bits(stream);
     if (!err) return 0;
-    return fail(HIDEGS_E_ASYNC, std::string(what) + ": not run -- an earlier sort's hot-tile partition queue failed (error " +
-                                    std::to_string(err) + ((err & 1u) ? ", job slots exhausted" : "") +
+    return fail(HIDEGS_E_ASYNC, std::string(what) + ": not run -- an earlier sort on this stream failed in its hot-tile "
+                                    "partition queue (error " + std::to_string(err) +
+                                    ((err & 1u) ? ", job slots exhausted" : "") +
                                     ((err & 4u) ? ", a worker gave up waiting" : "") +
                                     "): that sort's output is not sorted");
 }

@@ -254,7 +254,7 @@ int masked_adam_multi(const hidegs_adam_tensor* tensors, int count, hipStream_t 
 
 extern "C" int hidegs_masked_adam_multi(const hidegs_adam_tensor* tensors, int count, void* stream)
 {
-    if (int rc = hidegs::take_async_error("hidegs_masked_adam_multi")) return rc;
+    if (int rc = hidegs::take_async_error("hidegs_masked_adam_multi", hidegs::as_stream(stream))) return rc;
     return hidegs::masked_adam_multi(tensors, count, hidegs::as_stream(stream));
 }
 
@@ -262,7 +262,7 @@ extern "C" int hidegs_masked_adam(float* param, const float* grad, float* exp_av
                                   const unsigned char* relevant, long long rows, int width, double lr, double beta1,
                                   double beta2, double eps, double weight_decay, long long step, void* stream)
 {
-    if (int rc = hidegs::take_async_error("hidegs_masked_adam")) return rc;
+    if (int rc = hidegs::take_async_error("hidegs_masked_adam", hidegs::as_stream(stream))) return rc;
     hidegs_adam_tensor t;
     t.param = param;
     t.grad = grad;

@@ -36,17 +36,20 @@ bool debug_enabled();
 // Reads and clears it in one device-side exchange.
 int queue_error(hipStream_t stream, int clear, uint32_t* flags);
 
-// Asynchronous error word: one u32 of mapped, coherent pinned host memory that a sort's last kernel
-// sets (system-scope store) when its partition queue failed, so that the failure surfaces without a
-// host synchronisation.  async_error_slot() returns its device address (NULL if it could not be
-// allocated, or the first request comes from a stream being captured into a graph: then only the debug
+// Asynchronous error words: one u32 per stream in a page of mapped, coherent pinned host memory.  A
+// sort's last kernel ORs its partition queue's error bits into its stream's word (system-scope vector
+// stores), so that the failure surfaces without a host synchronisation.  The page is allocated by the
+// first entry-point call of any kind that does not come from a stream being captured into a graph.
+// async_error_slot() returns the device address of `stream`'s word (NULL if the page does not exist:
+// it could not be allocated, or every call so far came from a capturing stream; then only the debug
 // mode and hidegs_queue_error report that call's queue errors).
 uint32_t* async_error_slot(hipStream_t stream);
-// Called first by every compute entry point: a set word is taken (exchanged with 0) and turned into
-// HIDEGS_E_ASYNC with its message, so the call after a failed sort fails loudly instead of running.
-int take_async_error(const char* what);
-// The word's bits, taken (exchanged with 0); 0 when none are pending.
-uint32_t take_async_bits();
+// Called first by every compute entry point: if `stream`'s word is set it is taken (exchanged with 0)
+// and turned into HIDEGS_E_ASYNC with its message, so a call on the stream of a failed sort, made once
+// that sort's last kernel has run, fails loudly instead of running.
+int take_async_error(const char* what, hipStream_t stream);
+// `stream`'s word's bits, taken (exchanged with 0); 0 when none are pending.
+uint32_t take_async_bits(hipStream_t stream);
 
 // 256-byte aligned carving of one caller-provided scratch buffer.
 constexpr size_t kAlign = 256;

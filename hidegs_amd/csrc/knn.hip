@@ -926,7 +926,7 @@ extern "C" {
 int hidegs_dist_cuda2(hidegs_alloc_fn scratch_buffer, void* alloc_user, int P, const float* points, float* mean_dists,
                       void* stream)
 {
-    if (int rc = hidegs::take_async_error("hidegs_dist_cuda2")) return rc;
+    if (int rc = hidegs::take_async_error("hidegs_dist_cuda2", hidegs::as_stream(stream))) return rc;
     return hidegs::dist_cuda2(scratch_buffer, alloc_user, P, points, mean_dists, hidegs::as_stream(stream));
 }
 

@@ -1010,7 +1010,10 @@ constexpr bool kDeferPieces = HIDEGS_DEFER_PIECES != 0;
 #ifndef HIDEGS_WIDE_SCOUTS
 #define HIDEGS_WIDE_SCOUTS 0  // 1: scouts hand hot tiles of <= kWideCap pairs to the queue as WIDE jobs (slower: DESIGN.md)
 #endif
-constexpr uint32_t kMaxPolls = 1u << 22;
+#ifndef HIDEGS_MAX_POLLS
+#define HIDEGS_MAX_POLLS (1u << 22)  // a waiting worker gives up after this many polls (~13 s at the longest backoff)
+#endif
+constexpr uint32_t kMaxPolls = HIDEGS_MAX_POLLS;
 enum : uint32_t { J_EXIT = 0, J_SMALL, J_COPY, J_REDUCE, J_HIST, J_SCATTER, J_GLOBAL, J_WIDE };
 enum : int { Q_HEAD, Q_RESERVE, Q_DONE, Q_NREC, Q_POOL, Q_ERROR, Q_NPIECE, Q_COUNTERS = 8 };
 constexpr int kCtlStride = 32;  // one 128-byte line per counter: polls of one do not queue behind another's atomics
@@ -2469,11 +2472,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HIDEGS_P
 {
     __shared__ __attribute__((aligned(16))) SegLds lds;
     __shared__ uint32_t s_and[kWavesPerBlock], s_or[kWavesPerBlock], s_max[kWavesPerBlock];
-    // the queue has drained (stream order): its error word is final.  A set word goes to the mapped
-    // host word (a vector store at system scope), which the next entry-point call takes as HIDEGS_E_ASYNC.
+    // the queue has drained (stream order): its error word is final.  A set word is ORed into the
+    // stream's mapped host word (vector load and store at system scope), which an entry-point call on
+    // this stream takes as HIDEGS_E_ASYNC.  Not an atomic OR (system-scope atomics on host memory are
+    // not relied on): earlier sorts on the stream have finished, so only the host's take can fall
+    // between the load and the store, and then those bits are reported twice -- never lost.
     if (async_err && blockIdx.x == 0 && threadIdx.x == 0) {
         const uint32_t err = q_peek(&q.ctl[kCtlStride * Q_ERROR]);
-        if (err) __hip_atomic_store(async_err, err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (err) {
+            const uint32_t old = __hip_atomic_load(async_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(async_err, old | err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     const uint32_t np = min(q.ctl[kCtlStride * Q_NPIECE], q.piece_cap);
     for (uint32_t p = blockIdx.x; p < np; p += gridDim.x) {
@@ -2775,8 +2784,8 @@ int queue_error(hipStream_t stream, int clear, uint32_t* flags)
             hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess)
         return fail(HIDEGS_E_HIP, "queue_error: readback failed");
-    // the asynchronous copy of the same failures: reported here and taken with the clear
-    if (clear) v |= take_async_bits();
+    // the asynchronous copy of the same failures on this stream: reported here and taken with the clear
+    if (clear) v |= take_async_bits(stream);
     *flags = v;
     return 0;
 }
@@ -2847,7 +2856,7 @@ size_t hidegs_scan_scratch_bytes(long long n) { return n > 0 ? hidegs::inclusive
 int hidegs_inclusive_scan_u32(void* scratch, size_t scratch_bytes, const uint32_t* in, uint32_t* out, long long n,
                               void* stream)
 {
-    if (int rc = hidegs::take_async_error("hidegs_inclusive_scan_u32")) return rc;
+    if (int rc = hidegs::take_async_error("hidegs_inclusive_scan_u32", hidegs::as_stream(stream))) return rc;
     return hidegs::inclusive_scan_u32(scratch, scratch_bytes, in, out, n, hidegs::as_stream(stream));
 }
 
@@ -2856,7 +2865,7 @@ int hidegs_sort_pairs_u64(void* scratch, size_t scratch_bytes, const uint64_t* k
                           const uint32_t* vals_in, uint32_t* vals_out, long long n, int begin_bit, int end_bit,
                           void* stream)
 {
-    if (int rc = hidegs::take_async_error("hidegs_sort_pairs_u64")) return rc;
+    if (int rc = hidegs::take_async_error("hidegs_sort_pairs_u64", hidegs::as_stream(stream))) return rc;
     return hidegs::sort_pairs_u64(scratch, scratch_bytes, keys_in, keys_out, vals_in, vals_out, n, begin_bit, end_bit,
                                   hidegs::as_stream(stream));
 }
@@ -2866,7 +2875,7 @@ int hidegs_sort_pairs_u32(void* scratch, size_t scratch_bytes, const uint32_t* k
                           const uint32_t* vals_in, uint32_t* vals_out, long long n, int begin_bit, int end_bit,
                           void* stream)
 {
-    if (int rc = hidegs::take_async_error("hidegs_sort_pairs_u32")) return rc;
+    if (int rc = hidegs::take_async_error("hidegs_sort_pairs_u32", hidegs::as_stream(stream))) return rc;
     return hidegs::sort_pairs_u32(scratch, scratch_bytes, keys_in, keys_out, vals_in, vals_out, n, begin_bit, end_bit,
                                   hidegs::as_stream(stream));
 }
@@ -2875,7 +2884,7 @@ int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* 
                            const uint32_t* vals_in, uint32_t* vals_out, long long n, int num_tiles, uint32_t* ranges,
                            void* stream)
 {
-    if (int rc = hidegs::take_async_error("hidegs_sort_tile_pairs")) return rc;
+    if (int rc = hidegs::take_async_error("hidegs_sort_tile_pairs", hidegs::as_stream(stream))) return rc;
     return hidegs::sort_tile_pairs(scratch, scratch_bytes, keys_in, keys_out, vals_in, vals_out, n, num_tiles, ranges,
                                    hidegs::as_stream(stream));
 }
@@ -2883,7 +2892,7 @@ int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* 
 int hidegs_identify_tile_ranges(const uint64_t* sorted_keys, long long n, uint32_t* ranges, int num_tiles,
                                 void* stream)
 {
-    if (int rc = hidegs::take_async_error("hidegs_identify_tile_ranges")) return rc;
+    if (int rc = hidegs::take_async_error("hidegs_identify_tile_ranges", hidegs::as_stream(stream))) return rc;
     return hidegs::identify_tile_ranges(sorted_keys, n, ranges, num_tiles, hidegs::as_stream(stream));
 }
 

@@ -156,7 +156,7 @@ constexpr long long kMaxWire = (long long)kBlock * kVec * 0x7fffffffLL;
 extern "C" int hidegs_bf16_pack(const float* src, uint16_t* dst, long long n, long long n_padded, void* stream)
 {
     using namespace hidegs;
-    if (int rc = take_async_error("hidegs_bf16_pack")) return rc;
+    if (int rc = take_async_error("hidegs_bf16_pack", hidegs::as_stream(stream))) return rc;
     if (n < 0 || n_padded < n || n_padded > kMaxWire) return fail(HIDEGS_E_ARG, "bf16_pack: bad sizes");
     if (n_padded == 0) return 0;
     if (!dst || (n > 0 && !src)) return fail(HIDEGS_E_ARG, "bf16_pack: NULL pointer");
@@ -169,7 +169,7 @@ extern "C" int hidegs_bf16_pack(const float* src, uint16_t* dst, long long n, lo
 extern "C" int hidegs_bf16_sum_ranks(const uint16_t* parts, int world, long long chunk, uint16_t* out, void* stream)
 {
     using namespace hidegs;
-    if (int rc = take_async_error("hidegs_bf16_sum_ranks")) return rc;
+    if (int rc = take_async_error("hidegs_bf16_sum_ranks", hidegs::as_stream(stream))) return rc;
     if (world < 1 || chunk < 0 || chunk > kMaxWire) return fail(HIDEGS_E_ARG, "bf16_sum_ranks: bad sizes");
     if (chunk == 0) return 0;
     if (!parts || !out) return fail(HIDEGS_E_ARG, "bf16_sum_ranks: NULL pointer");
@@ -183,7 +183,7 @@ extern "C" int hidegs_bf16_sum_ranks(const uint16_t* parts, int world, long long
 extern "C" int hidegs_bf16_unpack(const uint16_t* src, float* dst, long long n, void* stream)
 {
     using namespace hidegs;
-    if (int rc = take_async_error("hidegs_bf16_unpack")) return rc;
+    if (int rc = take_async_error("hidegs_bf16_unpack", hidegs::as_stream(stream))) return rc;
     if (n < 0 || n > kMaxWire) return fail(HIDEGS_E_ARG, "bf16_unpack: bad size");
     if (n == 0) return 0;
     if (!src || !dst) return fail(HIDEGS_E_ARG, "bf16_unpack: NULL pointer");
@@ -196,7 +196,7 @@ extern "C" int hidegs_bf16_unpack(const uint16_t* src, float* dst, long long n, 
 extern "C" int hidegs_mask_pack(const unsigned char* mask, long long n, unsigned char* bits, void* stream)
 {
     using namespace hidegs;
-    if (int rc = take_async_error("hidegs_mask_pack")) return rc;
+    if (int rc = take_async_error("hidegs_mask_pack", hidegs::as_stream(stream))) return rc;
     if (n < 0 || n > (long long)kBlock * 8 * 0x7fffffffLL) return fail(HIDEGS_E_ARG, "mask_pack: bad size");
     if (n == 0) return 0;
     if (!mask || !bits) return fail(HIDEGS_E_ARG, "mask_pack: NULL pointer");
@@ -210,7 +210,7 @@ extern "C" int hidegs_mask_union_count(const unsigned char* bits, int ranks, lon
                                        float* count, void* stream)
 {
     using namespace hidegs;
-    if (int rc = take_async_error("hidegs_mask_union_count")) return rc;
+    if (int rc = take_async_error("hidegs_mask_union_count", hidegs::as_stream(stream))) return rc;
     if (ranks < 1 || n < 0 || n > (long long)kBlock * 0x7fffffffLL) return fail(HIDEGS_E_ARG, "mask_union_count: bad sizes");
     if (n == 0) return 0;
     if (!bits || !any || !count) return fail(HIDEGS_E_ARG, "mask_union_count: NULL pointer");

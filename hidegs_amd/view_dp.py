@@ -50,9 +50,26 @@ the default 64 MiB buckets) whatever the arena's size, instead of ~6 B per arena
 dense bucket's rows are updated as soon as that bucket's all-reduce lands, while the later
 buckets are still reducing (SURVEY §8(e) E2's overlap; the backward that would also overlap it is
 not built here).
+
+Failure detection ("DP: fail fast on RCCL error").  Every collective is issued
+asynchronously and waited on through one helper, so no wait is unbounded and a rank that stops
+participating (stalled, crashed) turns into a RuntimeError naming the collective -- visibility
+all-gather, bucket i of k (fp32 all-reduce, bf16 all-to-all or all-gather) or the MAX all-reduce --
+on the ranks still waiting:
+* host tensors (gloo): each wait is bounded by `timeout` (seconds, default 300) and raises when it
+  expires.  The process group's own timeout (`init_process_group(timeout=...)`) still bounds the
+  abandoned operation, so a process exiting after the error takes up to that long to tear down.
+* device tensors (RCCL): a wait only makes the compute stream wait on the collective's stream --
+  the host never blocks, which is what lets the bucket pipeline overlap.  A collective that never
+  completes is caught by the process group's watchdog after the process group's timeout, which aborts
+  the communicators and ends the process (TORCH_NCCL_ASYNC_ERROR_HANDLING, on by default): pass an
+  explicit `timeout` to init_process_group (bench.py does).  `blocking=True` bounds the host wait by
+  `timeout` on device tensors too and raises the same RuntimeError, at the price of a host wait per
+  collective (the bucket overlap then depends on the host keeping ahead).
 """
 from __future__ import annotations
 
+import datetime
 from dataclasses import dataclass
 from typing import Dict, Iterable, List, Optional, Union
 
@@ -157,9 +174,12 @@ class _Bucket:
     flight: start() issues the first collective, mid() the second (bf16 only: the fp32 sum of this
     rank's chunk between the two), finish() waits and leaves the summed values in `view` (fp32)."""
 
-    def __init__(self, view: torch.Tensor, group, transport: str, world: int, rank: int):
+    def __init__(self, view: torch.Tensor, group, transport: str, world: int, rank: int, wait=None,
+                 label: str = "bucket"):
         self.view, self.group, self.transport, self.world, self.rank = view, group, transport, world, rank
         self.work = None
+        self.label = label
+        self._wait = wait or (lambda work, what: work.wait())
 
     def start(self) -> int:
         if self.transport == "fp32":
@@ -183,7 +203,7 @@ class _Bucket:
     def mid(self) -> int:
         if self.transport == "fp32":
             return 0
-        self.work.wait()
+        self._wait(self.work, f"{self.label}: bf16 all-to-all")
         parts = self.recv.view(self.world, self.chunk)
         if parts.is_cuda:  # one pass over the w rows (csrc/wire.hip), the same bits as below
             mine = wire.bf16_sum_ranks(parts)
@@ -200,7 +220,8 @@ class _Bucket:
         return 1
 
     def finish(self) -> None:
-        self.work.wait()
+        self._wait(self.work, f"{self.label}: " + ("fp32 SUM all-reduce" if self.transport == "fp32"
+                                                   else "bf16 all-gather"))
         if self.transport == "bf16":
             flat = self.view.reshape(-1)  # a view: the bucket is a contiguous slice
             if flat.is_cuda:
@@ -225,13 +246,17 @@ class ViewDPExchange:
 
     def __init__(self, group: Optional[dist.ProcessGroup] = None, bucket_bytes: int = 64 << 20,
                  compact_below: float = 0.75, debug: bool = False, transport: str = "fp32",
-                 force_collectives: bool = False):
+                 force_collectives: bool = False, timeout: Optional[float] = 300.0, blocking: bool = False):
         if bucket_bytes < 4:
             raise ValueError("bucket_bytes must hold at least one fp32 value")
         if not 0.0 <= compact_below <= 1.0:
             raise ValueError("compact_below is a fraction of rows in [0, 1]")
         if transport not in TRANSPORTS:
             raise ValueError(f"transport must be one of {TRANSPORTS}")
+        if timeout is not None and not timeout > 0:
+            raise ValueError("timeout is a positive number of seconds (or None: the process group's own)")
+        self.timeout = None if timeout is None else float(timeout)
+        self.blocking = bool(blocking)
         self.transport = transport
         self.group = group
         self.bucket_bytes = int(bucket_bytes)
@@ -246,6 +271,24 @@ class ViewDPExchange:
         """One rank and nothing forced: every sum is its input, no collective is issued."""
         return dist.get_world_size(self.group) == 1 and not self.force_collectives
 
+    def _wait(self, work, what: str, cuda: bool) -> None:
+        """Wait for one collective: bounded on the host (gloo, or blocking=True) or a stream wait (RCCL,
+        bounded by the process group's watchdog); a timeout or a failed peer raises RuntimeError naming it."""
+        bounded = self.timeout is not None and (not cuda or self.blocking)
+        try:
+            done = work.wait(datetime.timedelta(seconds=self.timeout)) if bounded else work.wait()
+        except Exception as e:  # noqa: BLE001 -- re-raised with the collective named
+            raise RuntimeError(self._failure(what, bounded, e)) from e
+        if done is False:
+            raise RuntimeError(self._failure(what, bounded, None))
+
+    def _failure(self, what: str, bounded: bool, err) -> str:
+        rank, world = dist.get_rank(self.group), dist.get_world_size(self.group)
+        limit = f" (waited at most {self.timeout:g} s)" if bounded else ""
+        cause = f": {type(err).__name__}: {err}" if err is not None else ""
+        return (f"view-DP exchange: {what} did not complete on rank {rank} of {world}{limit}{cause}; another rank "
+                "stopped participating or failed -- the replicas can no longer agree, end this process")
+
     # ---- visibility -------------------------------------------------------------
     def gather_visibility(self, visible: torch.Tensor):
         """(union bool (N,), view_count float32 (N,1)) over every rank's mask; one all-gather."""
@@ -257,7 +300,8 @@ class ViewDPExchange:
         cuda = visible.is_cuda
         bits = wire.mask_pack(visible.contiguous()) if cuda else pack_mask(visible)
         flat = bits.new_empty((world * bits.numel(),))
-        dist.all_gather_into_tensor(flat, bits, group=self.group)
+        self._wait(dist.all_gather_into_tensor(flat, bits, group=self.group, async_op=True),
+                   "visibility all-gather", cuda)
         self.last.collectives += 1
         if cuda:  # one pass (csrc/wire.hip), the same result as the torch definition below
             return wire.mask_union_count(flat.view(world, bits.numel()), visible.numel())
@@ -266,8 +310,16 @@ class ViewDPExchange:
         return count > 0, count.to(torch.float32).unsqueeze(1)
 
     # ---- leaf gradients -----------------------------------------------------------
-    def _bucket(self, view: torch.Tensor) -> _Bucket:
-        return _Bucket(view, self.group, self.transport, dist.get_world_size(self.group), dist.get_rank(self.group))
+    def _bucket(self, view: torch.Tensor, label: str = "bucket") -> _Bucket:
+        cuda = view.is_cuda
+        return _Bucket(view, self.group, self.transport, dist.get_world_size(self.group), dist.get_rank(self.group),
+                       wait=lambda work, what: self._wait(work, what, cuda), label=label)
+
+    @staticmethod
+    def _label_buckets(buckets: List[_Bucket], what: str) -> List[_Bucket]:
+        for i, b in enumerate(buckets):
+            b.label = f"{what} bucket {i + 1} of {len(buckets)} ({b.view.numel() * 4 / 2**20:.1f} MiB fp32)"
+        return buckets
 
     def _run_buckets(self, buckets: List[_Bucket], after=None) -> None:
         """fp32: every bucket's all-reduce issued at once (in place: no extra memory).  bf16: the first
@@ -297,11 +349,12 @@ class ViewDPExchange:
             if after is not None:
                 after(i)
 
-    def _all_reduce_buckets(self, flat: torch.Tensor) -> None:
+    def _all_reduce_buckets(self, flat: torch.Tensor, what: str = "gradient") -> None:
         if self._solo():  # the sum over one rank is the tensor itself
             return
         per = max(1, self.bucket_bytes // flat.element_size())
-        self._run_buckets([self._bucket(flat[s:s + per]) for s in range(0, flat.numel(), per)])
+        self._run_buckets(self._label_buckets([self._bucket(flat[s:s + per]) for s in range(0, flat.numel(), per)],
+                                              what))
 
     def sum_gradients(self, grads: Union[GradArena, Iterable[torch.Tensor]],
                       union: Optional[torch.Tensor] = None) -> None:
@@ -367,7 +420,7 @@ class ViewDPExchange:
         for g, w in zip(tensors, widths):
             torch.index_select(g.reshape(n, w), 0, rows, out=packed[off:off + rows.numel() * w].view(-1, w))
             off += rows.numel() * w
-        self._all_reduce_buckets(packed)
+        self._all_reduce_buckets(packed, "compacted gradient")
         off = 0
         for g, w in zip(tensors, widths):
             g.reshape(n, w).index_copy_(0, rows, packed[off:off + rows.numel() * w].view(-1, w))
@@ -380,7 +433,8 @@ class ViewDPExchange:
         if not stats or self._solo():
             return
         flat = torch.cat([s.reshape(-1).to(torch.float32) for s in stats])
-        dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=self.group)
+        self._wait(dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=self.group, async_op=True),
+                   "MAX all-reduce of the per-step maxima", flat.is_cuda)
         self.last.collectives += 1
         off = 0
         for s in stats:
@@ -453,6 +507,8 @@ class ViewDPExchange:
                     r1 = min(n, r0 + rows)
                     spans.append((name, r0, r1))
                     buckets.append(self._bucket(view[r0:r1]))
+            for (name, r0, r1), b in zip(spans, self._label_buckets(buckets, "gradient")):
+                b.label += f" = {name} rows {r0}..{r1}"
             plans = []
 
             def step_rows(i):

@@ -59,13 +59,43 @@ extern "C" {
 typedef char* (*hidegs_alloc_fn)(void* user, size_t nbytes);
 
 /*
+ * ABI deltas.  The three rasterizer entry points below keep the parameters of the interfaces they
+ * replace (HR/cuda_rasterizer/rasterizer.h:24-118), in the same order and under the same names, except
+ * for the parameters listed here.  A dropped parameter is one the reference glue (HR/rasterize_points.cu)
+ * always passes with the same value; the value given is the one this ABI assumes.  An added parameter
+ * has no reference counterpart.  tests/test_abi.py parses these lines and checks them against the
+ * reference signatures and the prototypes below.
+ * Line format:  DELTA <entry point> <dropped|added|renamed|retyped> <reference name>[ -> <name here>] : <meaning>
+ *
+ * DELTA hidegs_rasterize_forward dropped rects : non-null in the glue (rasterize_points.cu:94,141), so the rect-bounded tile path (forward.cu:390-395) is always taken; the rects are per-call scratch (the glue never returns them)
+ * DELTA hidegs_rasterize_forward dropped boxmin : NULL in the glue (rasterize_points.cu:142): no bounding-box cull
+ * DELTA hidegs_rasterize_forward dropped boxmax : NULL in the glue (rasterize_points.cu:143): no bounding-box cull
+ * DELTA hidegs_rasterize_forward dropped skyboxnum : the default 0 (rasterizer.h:69; the glue passes nothing after debug)
+ * DELTA hidegs_rasterize_forward dropped biglimit : the default INFINITY (rasterizer.h:72): no cull of large Gaussians
+ * DELTA hidegs_rasterize_forward dropped on_cpu : the default false (rasterizer.h:73): device buffers only
+ * DELTA hidegs_rasterize_forward added alloc_user : the user argument handed to the three hidegs_alloc_fn callbacks (the C form of a capturing std::function)
+ * DELTA hidegs_rasterize_forward renamed depth -> out_invdepth : the inverse-depth image, NULL when do_depth is false (rasterize_points.cu:76-82,135)
+ * DELTA hidegs_rasterize_forward retyped geometryBuffer : std::function<char*(size_t)> -> hidegs_alloc_fn (binningBuffer and imageBuffer likewise)
+ * DELTA hidegs_rasterize_forward retyped prefiltered : bool -> int (render_geo and debug likewise)
+ * DELTA hidegs_rasterize_forward retyped stream : the glue passes nothing, i.e. the legacy default stream (rasterizer.h:70) -> the caller's current stream
+ * DELTA hidegs_rasterize_forward retyped num_rendered : the glue passes nothing (nullptr) and takes the pair count from the return value (rasterize_points.cu:108) -> [host] out-pointer written with the count; the return value is the status
+ * DELTA hidegs_rasterize_backward dropped dL_dconic : (fullP, 2, 2) zeros the glue allocates and discards (rasterize_points.cu:200,264); here an internal intermediate
+ * DELTA hidegs_rasterize_backward dropped dL_dinvdepth : per-Gaussian (fullP, 1) zeros the glue allocates when dL_invdepths is given and discards (rasterize_points.cu:206-216,267); here an internal intermediate
+ * DELTA hidegs_rasterize_backward added h_var_bwd : anti-aliasing variance of the covariance backward, a constant 0.3 in the reference (backward.cu:211; the forward uses 0.1, forward.cu:356); the binding passes _C.H_VAR_BWD (0.3)
+ * DELTA hidegs_rasterize_backward added stream : the caller's current stream (the reference launches on the legacy default stream)
+ * DELTA hidegs_rasterize_backward retyped render_geo : bool -> int (debug likewise)
+ * DELTA hidegs_mark_visible added stream : the caller's current stream (the reference launches on the legacy default stream)
+ * DELTA hidegs_mark_visible retyped present : bool* -> unsigned char*, one byte per Gaussian, 0 or 1
+ */
+
+/*
  * Forward rasterization (P Gaussians, SH degree D, M SH coefficients per Gaussian).
  * Argument meaning as RasterizeGaussiansCUDA; hierarchy inputs (indices, parent_indices,
  * ts, kids) may be NULL.  *num_rendered [host] receives the Gaussian/tile pair count
  * (one host readback).  Not built in this release: returns HIDEGS_E_UNSUPPORTED.
  */
 int hidegs_rasterize_forward(
-    hidegs_alloc_fn geometry_buffer, hidegs_alloc_fn binning_buffer, hidegs_alloc_fn image_buffer, void* alloc_user,
+    hidegs_alloc_fn geometryBuffer, hidegs_alloc_fn binningBuffer, hidegs_alloc_fn imageBuffer, void* alloc_user,
     int P, int D, int M,
     const float* background, int width, int height,
     const int* indices, const int* parent_indices, const float* ts, const int* kids,
@@ -93,7 +123,7 @@ int hidegs_rasterize_backward(
     const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* campos,
     float tan_fovx, float tan_fovy, const int* radii, float h_var_bwd,
     char* geom_buffer, char* binning_buffer, char* image_buffer,
-    const float* dL_dpix, const float* dL_dout_all_map, const float* dL_dout_plane_depth, const float* dL_dinvdepth,
+    const float* dL_dpix, const float* dL_dout_all_map, const float* dL_dout_plane_depth, const float* dL_invdepths,
     float* dL_dmean2D, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
     float* dL_dsh, float* dL_dscale, float* dL_drot, float* dL_dall_map,
     int render_geo, int debug, void* stream);

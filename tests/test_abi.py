@@ -25,6 +25,73 @@ def header_functions():
     return out
 
 
+def header_parameters():
+    """{entry point: [parameter names in order]} from the prototypes of include/hidegs.h."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"^(?!typedef)[A-Za-z_][\w\s\*]*?\b(hidegs_\w+)\s*\(([^;]*?)\)\s*;", text, flags=re.M):
+        params = m.group(2).strip()
+        names = [] if params in ("", "void") else [re.findall(r"\w+", p)[-1] for p in params.split(",")]
+        out[m.group(1)] = names
+    return out
+
+
+# The replaced interfaces' parameter names, in order: CudaRasterizer::Rasterizer::markVisible, ::forward and
+# ::backward of the reference (submodules/hierarchy-rasterizer/cuda_rasterizer/rasterizer.h:24-29, 33-73, 75-117).
+REFERENCE_PARAMETERS = {
+    "hidegs_mark_visible": ["P", "means3D", "viewmatrix", "projmatrix", "present"],
+    "hidegs_rasterize_forward": [
+        "geometryBuffer", "binningBuffer", "imageBuffer", "P", "D", "M", "background", "width", "height", "indices",
+        "parent_indices", "ts", "kids", "means3D", "shs", "colors_precomp", "all_map", "opacities", "scales",
+        "scale_modifier", "rotations", "cov3D_precomp", "viewmatrix", "projmatrix", "cam_pos", "tan_fovx", "tan_fovy",
+        "prefiltered", "out_color", "depth", "out_observe", "out_all_map", "out_plane_depth", "render_geo", "radii",
+        "rects", "boxmin", "boxmax", "debug", "skyboxnum", "stream", "num_rendered", "biglimit", "on_cpu"],
+    "hidegs_rasterize_backward": [
+        "P", "D", "M", "R", "background", "all_map_pixels", "width", "height", "indices", "parent_indices", "ts",
+        "kids", "means3D", "shs", "colors_precomp", "all_maps", "scales", "opacities", "rotations", "scale_modifier",
+        "cov3D_precomp", "viewmatrix", "projmatrix", "campos", "tan_fovx", "tan_fovy", "radii", "geom_buffer",
+        "binning_buffer", "image_buffer", "dL_dpix", "dL_dout_all_map", "dL_dout_plane_depth", "dL_invdepths",
+        "dL_dmean2D", "dL_dconic", "dL_dopacity", "dL_dcolor", "dL_dinvdepth", "dL_dmean3D", "dL_dcov3D", "dL_dsh",
+        "dL_dscale", "dL_drot", "dL_dall_map", "render_geo", "debug"],
+}
+
+
+def header_deltas():
+    """[(entry point, kind, reference name, name here or None, meaning)] from the header's DELTA lines."""
+    pat = re.compile(r"^\s*\*\s*DELTA (\w+) (dropped|added|renamed|retyped) (\w+)(?: -> (\w+))? : (.+)$", re.M)
+    return [m.groups() for m in pat.finditer(open(HEADER).read())]
+
+
+def test_abi_deltas_name_exactly_the_parameters_that_differ():
+    """The header's DELTA block lists every parameter the ABI drops, adds or renames against
+    rasterizer.h:24-118 -- no more, no fewer -- and the other parameters keep the reference's order."""
+    ours, deltas = header_parameters(), header_deltas()
+    assert {d[0] for d in deltas} == set(REFERENCE_PARAMETERS)
+    for fn, ref in REFERENCE_PARAMETERS.items():
+        mine = [d for d in deltas if d[0] == fn]
+        renamed = {d[2]: d[3] for d in mine if d[1] == "renamed"}
+        assert all(renamed.values()), f"{fn}: a rename names its new parameter"
+        ref_here = [renamed.get(p, p) for p in ref]
+        dropped = {d[2] for d in mine if d[1] == "dropped"}
+        added = {d[2] for d in mine if d[1] == "added"}
+        assert dropped == set(ref_here) - set(ours[fn]), fn
+        assert added == set(ours[fn]) - set(ref_here), fn
+        assert [p for p in ref_here if p not in dropped] == [p for p in ours[fn] if p not in added], \
+            f"{fn}: the shared parameters are not in the reference's order"
+        for d in mine:
+            if d[1] == "retyped":
+                assert d[2] in ours[fn], f"{fn}: retyped {d[2]} is not a parameter"
+            assert len(d[4]) > 10, f"{fn} {d[2]}: no meaning given"
+    by = lambda fn, kind: {d[2] for d in deltas if d[0] == fn and d[1] == kind}  # noqa: E731
+    # VERDICT r05 item 1: the values the glue fixes (rasterize_points.cu:94,141-144; rasterizer.h:64-73,106,109)
+    assert by("hidegs_rasterize_forward", "dropped") == {"rects", "boxmin", "boxmax", "skyboxnum", "biglimit", "on_cpu"}
+    assert by("hidegs_rasterize_backward", "dropped") == {"dL_dconic", "dL_dinvdepth"}
+    assert "h_var_bwd" in by("hidegs_rasterize_backward", "added")
+    text = {d[2]: d[4] for d in deltas if d[0] == "hidegs_rasterize_forward"}
+    assert "non-null" in text["rects"] and "NULL" in text["boxmin"] and "NULL" in text["boxmax"]
+    assert "0" in text["skyboxnum"] and "INFINITY" in text["biglimit"] and "false" in text["on_cpu"]
+
+
 def test_header_parses():
     fns = header_functions()
     assert {"hidegs_rasterize_forward", "hidegs_dist_cuda2", "hidegs_sort_pairs_u64", "hidegs_version"} <= set(fns)

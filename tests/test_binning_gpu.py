@@ -547,6 +547,62 @@ def test_queue_overflow_is_reported_not_silent():
     assert primitives.queue_error() == 0
 
 
+def test_async_failure_reported_on_its_own_stream_once_the_sort_has_run():
+    """When and where HIDEGS_E_ASYNC surfaces without any host synchronisation.  A failing
+    sort (the qcap build) returns 0 on stream A; the host then keeps calling a scan on A and on B.  The
+    calls on A run normally until the sort's last kernel has set A's word -- the call right after the
+    sort does not know yet -- then exactly one call on A returns HIDEGS_E_ASYNC without running; no call
+    on B ever does (one word per stream).  Printed: how many calls and milliseconds that took."""
+    import ctypes as C
+    import time
+
+    from hidegs_amd import _lib, build
+    var = _lib.load_library(build.variant_path("qcap"))
+    g = np.random.default_rng(13)
+    T = 1024
+    keys, _ = raster_like_keys(200_000, T, 5)
+    hot = (np.uint64(77) << np.uint64(32)) | g.uniform(0.5, 60.0, 300_000).astype(np.float32).view(
+        np.uint32).astype(np.uint64)
+    keys = np.concatenate([keys, hot])[g.permutation(500_000)]
+    kd, vd = u64(keys), u32(np.arange(keys.size, dtype=np.uint32))
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    ha, hb = sa.cuda_stream, sb.cuda_stream
+    xa = torch.ones(1000, dtype=torch.int32, device="cuda")
+    xb = torch.ones(1000, dtype=torch.int32, device="cuda")
+    tmp_a = torch.empty(var.hidegs_scan_scratch_bytes(1000), dtype=torch.uint8, device="cuda")
+    tmp_b = torch.empty_like(tmp_a)
+    flags = C.c_uint32(0)
+    assert var.hidegs_queue_error(ha, 1, C.byref(flags)) == 0
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sa):
+        rc, _, _, _ = _variant_sort_tile_pairs(var, kd, vd, T)
+    assert rc == 0
+    t0 = time.perf_counter()
+    calls_a, reported_at, reported_ms, rcs_b = 0, None, None, []
+    while time.perf_counter() - t0 < 20.0:
+        rc = var.hidegs_inclusive_scan_u32(tmp_a.data_ptr(), tmp_a.numel(), xa.data_ptr(), xa.data_ptr(), 1000, ha)
+        calls_a += 1
+        rcs_b.append(var.hidegs_inclusive_scan_u32(tmp_b.data_ptr(), tmp_b.numel(), xb.data_ptr(), xb.data_ptr(),
+                                                   1000, hb))
+        if rc == _lib.E_ASYNC:
+            reported_at, reported_ms = calls_a, 1e3 * (time.perf_counter() - t0)
+            assert b"on this stream" in var.hidegs_last_error() and b"job slots exhausted" in var.hidegs_last_error()
+            break
+        assert rc == 0
+        time.sleep(0.002)
+    print(f"HIDEGS_E_ASYNC on the sort's stream at call {reported_at} after the sort, {reported_ms:.1f} ms; "
+          f"{len(rcs_b)} calls on the other stream, none failed")
+    assert reported_at is not None, "the failure was never reported on its stream"
+    assert reported_at > 1, "reported by the very next call: the sort had already finished (not the case tested)"
+    assert all(r == 0 for r in rcs_b)
+    # taken once: the next call on A runs (inclusive scans of ones; every earlier call but one ran on A)
+    assert var.hidegs_inclusive_scan_u32(tmp_a.data_ptr(), tmp_a.numel(), xa.data_ptr(), xa.data_ptr(), 1000, ha) == 0
+    torch.cuda.synchronize()
+    assert var.hidegs_inclusive_scan_u32(tmp_b.data_ptr(), tmp_b.numel(), xb.data_ptr(), xb.data_ptr(), 1000, hb) == 0
+    assert var.hidegs_queue_error(ha, 1, C.byref(flags)) == 0 and flags.value & 1  # the sticky device word
+    assert var.hidegs_queue_error(ha, 1, C.byref(flags)) == 0 and flags.value == 0
+
+
 def test_debug_mode_passes_clean_sorts():
     """Debug mode on the product build: synchronising checks and the queue check, no false alarm."""
     g = np.random.default_rng(12)

@@ -139,6 +139,92 @@ def test_view_dp_collectives_on_rccl_forced_single_rank(transport, compact_below
         dist.destroy_process_group()
 
 
+def test_hot_tile_queue_beside_an_rccl_exchange_on_another_stream():
+    """Config 4's concurrency: the binning sort of a skewed view -- hot tiles, so the
+    partition queue's cross-workgroup hand-offs run -- on one stream and host thread, while the view-DP
+    exchange with its overlapped masked Adam step (every RCCL call forced on a one-rank group) runs on
+    another stream from the main thread, several iterations each, started together.  Every sort is
+    bit-identical to oracle/binning.py, the queue's error word stays clear, the next call on the sort's
+    stream does not raise HIDEGS_E_ASYNC, and the exchange still equals Adam.step on the union."""
+    import threading
+
+    import numpy as np
+
+    from hidegs_amd import primitives, synthetic
+    from hidegs_amd.optim import Adam
+    from hidegs_amd.view_dp import LEAF_WIDTHS, GradArena, ViewDPExchange
+    from oracle import binning
+
+    iters = 6
+    cam = synthetic.d2_camera(1920, 1080)
+    wl = synthetic.d2_binning_workload(synthetic.d2_scene(2_000_000, cam, seed=1000, cluster=(0.15, 0.1)), cam)
+    T = wl.num_tiles
+    ek, ev = binning.stable_sort_pairs(wl.keys.numpy().view(np.uint64), wl.values.numpy().view(np.uint32), 0,
+                                       32 + primitives.higher_msb(T))
+    er = binning.tile_ranges(ek, T)
+    ek_d, ev_d = torch.from_numpy(ek.view(np.int64)).cuda(), torch.from_numpy(ev.view(np.int32)).cuda()
+    er_d = torch.from_numpy(er.view(np.int32)).cuda().view(T, 2)
+    keys, vals = wl.keys.cuda(), wl.values.cuda()
+    primitives.queue_error(clear=True)
+
+    dist = _one_rank_nccl()
+    try:
+        n = 1_000_000
+        g = torch.Generator(device="cuda").manual_seed(21)
+        visible = torch.rand(n, device="cuda", generator=g) < 0.9
+        init = {k: torch.randn(n, w, device="cuda", generator=g) for k, w in LEAF_WIDTHS.items()}
+        grads = {k: torch.randn(n, w, device="cuda", generator=g) for k, w in LEAF_WIDTHS.items()}
+        pa = {k: torch.nn.Parameter(v.clone()) for k, v in init.items()}
+        pb = {k: torch.nn.Parameter(v.clone()) for k, v in init.items()}
+        opt_a = Adam(list(pa.values()), lr=0.01, eps=1e-15)
+        opt_b = Adam(list(pb.values()), lr=0.01, eps=1e-15)
+        arena = GradArena(n, device="cuda")
+        arena.attach(pb)
+        for k in LEAF_WIDTHS:
+            pa[k].grad = grads[k].clone()
+        for _ in range(iters):
+            opt_a.step(visible)
+        ex = ViewDPExchange(bucket_bytes=16 << 20, compact_below=0.0, force_collectives=True)
+        sort_stream, dp_stream = torch.cuda.Stream(), torch.cuda.Stream()
+        torch.cuda.synchronize()
+        start = threading.Barrier(2)
+        results, errors = [], []
+
+        def sorter():
+            try:
+                with torch.cuda.stream(sort_stream):
+                    start.wait()
+                    for _ in range(iters):
+                        results.append(primitives.sort_tile_pairs(keys, vals, T))
+            except Exception as e:  # noqa: BLE001 -- re-raised on the main thread
+                errors.append(e)
+
+        th = threading.Thread(target=sorter)
+        th.start()
+        with torch.cuda.stream(dp_stream):
+            start.wait()
+            for _ in range(iters):
+                for k in LEAF_WIDTHS:
+                    arena[k].copy_(grads[k])
+                ex.exchange_and_step(arena, visible, opt_b, pb)
+        th.join(120)
+        assert not th.is_alive() and not errors, errors
+        torch.cuda.synchronize()
+        assert len(results) == iters
+        for it, (ko, vo, r) in enumerate(results):
+            assert torch.equal(ko, ek_d) and torch.equal(vo, ev_d) and torch.equal(r, er_d), f"sort {it} differs"
+        assert primitives.queue_error() == 0
+        with torch.cuda.stream(sort_stream):  # raises RuntimeError on a pending HIDEGS_E_ASYNC
+            ko, vo, _ = primitives.sort_tile_pairs(keys, vals, T)
+        torch.cuda.synchronize()
+        assert torch.equal(vo, ev_d)
+        assert ex.last.collectives > len(LEAF_WIDTHS)
+        for k in LEAF_WIDTHS:
+            assert torch.equal(pa[k].detach(), pb[k].detach()), k
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.parametrize("transport", ["fp32", "bf16"])
 def test_exchange_and_step_on_rccl_forced_single_rank(transport):
     """The overlapped path on hardware (every bucket's collective issued, then per bucket its wait
