@@ -45,9 +45,8 @@ extern "C" {
 #define HIDEGS_E_HIP (-2)         /* HIP runtime or kernel error */
 #define HIDEGS_E_ALLOC (-3)       /* a buffer callback returned NULL for a non-zero request */
 #define HIDEGS_E_UNSUPPORTED (-4) /* entry point not built in this release */
-#define HIDEGS_E_ASYNC (-5)       /* not run: an earlier call's asynchronous check failed (a sort's partition
-                                     queue; see hidegs_queue_error) -- the reference's fail-fast contract
-                                     without a host synchronisation per sort */
+#define HIDEGS_E_ASYNC (-5)       /* not run: an earlier sort on the same stream failed asynchronously (its
+                                     partition queue; see hidegs_queue_error for when this is reported) */
 
 /*
  * Scratch allocator callback, the C form of the reference's std::function<char*(size_t)>
@@ -193,11 +192,19 @@ int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* 
  * hidegs_sort_tile_pairs, sticky per device since it was last cleared: bit 1 = job slots
  * exhausted, bit 4 = a queue worker gave up waiting.  Non-zero means some sort since the last
  * clear returned pairs that are not fully sorted.  Synchronises `stream`; clear != 0 resets it (one
- * device-side exchange, so no error raised meanwhile is lost) and also takes the asynchronous word below.
- * Outside debug mode a failing sort also sets a process-wide word in mapped host memory from its last
- * kernel; the next call of any compute entry point finds it set, clears it and returns HIDEGS_E_ASYNC
- * without running (no host synchronisation per sort).  In debug mode (hidegs_set_debug) every such
- * sort checks its own queue after synchronising and returns HIDEGS_E_HIP itself.
+ * device-side exchange, so no error raised meanwhile is lost) and also takes `stream`'s asynchronous
+ * word below.
+ * Asynchronous report (no host synchronisation per sort): outside debug mode a failing sort's last
+ * kernel ORs the failure into a word of mapped host memory that belongs to the sort's stream.  A later
+ * compute entry-point call on that stream, made once that kernel has run, finds the word set, takes it
+ * and returns HIDEGS_E_ASYNC without running.  The sort returns before its kernels run, so the call right
+ * after it normally does NOT see the failure yet; a call that already consumed the unsorted pairs (on
+ * the GPU) cannot be stopped by this report.  Calls on other streams never see it.  A caller that
+ * needs the failure before consuming the output must either run in debug mode (hidegs_set_debug:
+ * every sort synchronises, checks its own queue and returns HIDEGS_E_HIP itself) or call
+ * hidegs_queue_error at a synchronisation point it already has.  The word is allocated by the first
+ * entry-point call that is not made while its stream is captured into a graph; sorts captured before
+ * any such call report through debug mode and hidegs_queue_error only.
  */
 int hidegs_queue_error(void* stream, int clear, uint32_t* flags);
 
