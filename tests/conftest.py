@@ -23,6 +23,22 @@ def pytest_collection_modifyitems(config, items):
             item.add_marker(skip)
 
 
+def pytest_sessionfinish(session, exitstatus):
+    """With HIDEGS_MAPS_OUT set (tools/gpu_round6.sh), list the in-tree shared objects this
+    test process mapped -- the native code the run actually used (profiles/r06_evidence.md)."""
+    out = os.environ.get("HIDEGS_MAPS_OUT")
+    if not out:
+        return
+    root, seen = os.path.realpath(ROOT), set()
+    with open(f"/proc/{os.getpid()}/maps") as f:
+        for line in f:
+            path = line.split()[-1] if len(line.split()) >= 6 else ""
+            if path.startswith(root) and path.endswith(".so"):
+                seen.add(os.path.relpath(path, root))
+    with open(out, "w") as f:
+        f.write("\n".join(sorted(seen)) + "\n")
+
+
 @pytest.fixture(scope="session")
 def built_lib():
     """Build libhidegs.so in-tree if it is missing or stale (hipcc cross-compiles without a GPU)."""

@@ -362,7 +362,7 @@ def test_bf16_transport_is_its_definition_and_identical_on_every_rank(world, com
     assert wire * 2 == reduced and compacted == (compact_below > 0.0)
 
 
-EX_TIMEOUT, PG_TIMEOUT = 1.5, 8.0
+EX_TIMEOUT, PG_TIMEOUT = 1.5, 5.0
 
 
 def worker_fail(rank, world, port, scenario, q):
