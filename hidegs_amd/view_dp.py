@@ -318,7 +318,9 @@ class ViewDPExchange:
     @staticmethod
     def _label_buckets(buckets: List[_Bucket], what: str) -> List[_Bucket]:
         for i, b in enumerate(buckets):
-            b.label = f"{what} bucket {i + 1} of {len(buckets)} ({b.view.numel() * 4 / 2**20:.1f} MiB fp32)"
+            nb = b.view.numel() * 4
+            size = f"{nb / 2**20:.1f} MiB" if nb >= 1 << 20 else f"{nb / 2**10:.1f} KiB"
+            b.label = f"{what} bucket {i + 1} of {len(buckets)} ({size} fp32)"
         return buckets
 
     def _run_buckets(self, buckets: List[_Bucket], after=None) -> None:
