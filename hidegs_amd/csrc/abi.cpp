@@ -9,6 +9,7 @@
 #include <atomic>
 #include <mutex>
 #include <unordered_map>
+#include <utility>
 
 namespace hidegs {
 
@@ -37,14 +38,18 @@ static int not_built(const char* fn) { return fail(HIDEGS_E_UNSUPPORTED, std::st
 namespace {
 // One word per stream (a process-wide word reported thread A's failed sort on thread B's
 // unrelated call and let a second failure overwrite the first's bits).  Streams past the table share
-// word 0.  A stream handle that is destroyed and handed out again keeps its word.
+// the last word.  A stream handle that is destroyed and handed out again keeps its word.  A sort
+// captured into a graph writes word 0 instead: the graph may be replayed on any stream, so that word
+// is taken by the next call on ANY stream.
 constexpr int kAsyncWords = 1024;
+constexpr int kGraphWord = 0;
+constexpr int kOverflowWord = kAsyncWords - 1;
 std::once_flag g_async_once;
 std::atomic<uint32_t*> g_async_host{nullptr};    // mapped, coherent pinned page of kAsyncWords words
 std::atomic<uint32_t*> g_async_device{nullptr};  // its device address (published after the host page)
 std::mutex g_slot_mutex;
 std::unordered_map<hipStream_t, int> g_slot;  // stream -> word index, guarded by g_slot_mutex
-int g_next_slot = 1;
+int g_next_slot = kGraphWord + 1;
 
 bool capturing(hipStream_t stream)
 {
@@ -85,7 +90,7 @@ int slot_of(hipStream_t stream, bool create)
     auto it = g_slot.find(stream);
     if (it != g_slot.end()) return it->second;
     if (!create) return -1;
-    const int s = g_next_slot < kAsyncWords ? g_next_slot++ : 0;
+    const int s = g_next_slot < kOverflowWord ? g_next_slot++ : kOverflowWord;
     g_slot.emplace(stream, s);
     return s;
 }
@@ -95,23 +100,36 @@ uint32_t* async_error_slot(hipStream_t stream)
 {
     ensure_async_page(stream);
     uint32_t* d = g_async_device.load(std::memory_order_acquire);
-    return d ? d + slot_of(stream, true) : nullptr;
+    if (!d) return nullptr;
+    return d + (capturing(stream) ? kGraphWord : slot_of(stream, true));
 }
+
+namespace {
+// (bits of `stream`'s own word, bits of the graph word), both taken
+std::pair<uint32_t, uint32_t> take_words(hipStream_t stream)
+{
+    uint32_t* h = g_async_host.load(std::memory_order_acquire);
+    if (!h) return {0u, 0u};
+    const int s = slot_of(stream, false);
+    const uint32_t own = s < 0 ? 0u : __atomic_exchange_n(h + s, 0u, __ATOMIC_SEQ_CST);
+    return {own, __atomic_exchange_n(h + kGraphWord, 0u, __ATOMIC_SEQ_CST)};
+}
+}  // namespace
 
 uint32_t take_async_bits(hipStream_t stream)
 {
-    uint32_t* h = g_async_host.load(std::memory_order_acquire);
-    if (!h) return 0u;
-    const int s = slot_of(stream, false);
-    return s < 0 ? 0u : __atomic_exchange_n(h + s, 0u, __ATOMIC_SEQ_CST);
+    const auto w = take_words(stream);
+    return w.first | w.second;
 }
 
 int take_async_error(const char* what, hipStream_t stream)
 {
     ensure_async_page(stream);
-    const uint32_t err = take_async_bits(stream);
+    const auto w = take_words(stream);
+    const uint32_t err = w.first | w.second;
     if (!err) return 0;
-    return fail(HIDEGS_E_ASYNC, std::string(what) + ": not run -- an earlier sort on this stream failed in its hot-tile "
+    const char* who = w.first ? "an earlier sort on this stream" : "a sort replayed from a graph (any stream)";
+    return fail(HIDEGS_E_ASYNC, std::string(what) + ": not run -- " + who + " failed in its hot-tile "
                                     "partition queue (error " + std::to_string(err) +
                                     ((err & 1u) ? ", job slots exhausted" : "") +
                                     ((err & 4u) ? ", a worker gave up waiting" : "") +

@@ -40,15 +40,17 @@ int queue_error(hipStream_t stream, int clear, uint32_t* flags);
 // sort's last kernel ORs its partition queue's error bits into its stream's word (system-scope vector
 // stores), so that the failure surfaces without a host synchronisation.  The page is allocated by the
 // first entry-point call of any kind that does not come from a stream being captured into a graph.
-// async_error_slot() returns the device address of `stream`'s word (NULL if the page does not exist:
-// it could not be allocated, or every call so far came from a capturing stream; then only the debug
-// mode and hidegs_queue_error report that call's queue errors).
+// async_error_slot() returns the device address of `stream`'s word -- of the graph word when `stream`
+// is being captured (a graph may be replayed on any stream) -- or NULL if the page does not exist (it
+// could not be allocated, or every call so far came from a capturing stream; then only the debug mode
+// and hidegs_queue_error report that call's queue errors).
 uint32_t* async_error_slot(hipStream_t stream);
-// Called first by every compute entry point: if `stream`'s word is set it is taken (exchanged with 0)
-// and turned into HIDEGS_E_ASYNC with its message, so a call on the stream of a failed sort, made once
-// that sort's last kernel has run, fails loudly instead of running.
+// Called first by every compute entry point: if `stream`'s word (or the graph word) is set it is taken
+// (exchanged with 0) and turned into HIDEGS_E_ASYNC with its message, so a call on the stream of a failed
+// sort (any call, after a failed graph replay), made once that sort's last kernel has run, fails loudly
+// instead of running.
 int take_async_error(const char* what, hipStream_t stream);
-// `stream`'s word's bits, taken (exchanged with 0); 0 when none are pending.
+// `stream`'s word's bits and the graph word's, taken (exchanged with 0); 0 when none are pending.
 uint32_t take_async_bits(hipStream_t stream);
 
 // 256-byte aligned carving of one caller-provided scratch buffer.

@@ -45,8 +45,9 @@ extern "C" {
 #define HIDEGS_E_HIP (-2)         /* HIP runtime or kernel error */
 #define HIDEGS_E_ALLOC (-3)       /* a buffer callback returned NULL for a non-zero request */
 #define HIDEGS_E_UNSUPPORTED (-4) /* entry point not built in this release */
-#define HIDEGS_E_ASYNC (-5)       /* not run: an earlier sort on the same stream failed asynchronously (its
-                                     partition queue; see hidegs_queue_error for when this is reported) */
+#define HIDEGS_E_ASYNC (-5)       /* not run: an earlier sort on the same stream (or one replayed from a graph)
+                                     failed asynchronously in its partition queue; see hidegs_queue_error for
+                                     when this is reported */
 
 /*
  * Scratch allocator callback, the C form of the reference's std::function<char*(size_t)>
@@ -202,9 +203,11 @@ int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* 
  * the GPU) cannot be stopped by this report.  Calls on other streams never see it.  A caller that
  * needs the failure before consuming the output must either run in debug mode (hidegs_set_debug:
  * every sort synchronises, checks its own queue and returns HIDEGS_E_HIP itself) or call
- * hidegs_queue_error at a synchronisation point it already has.  The word is allocated by the first
- * entry-point call that is not made while its stream is captured into a graph; sorts captured before
- * any such call report through debug mode and hidegs_queue_error only.
+ * hidegs_queue_error at a synchronisation point it already has.  A sort captured into a graph cannot
+ * know the stream it will be replayed on: it reports to a graph word that the next compute call on ANY
+ * stream takes.  The words are allocated by the first entry-point call that is not made while its
+ * stream is captured into a graph; sorts captured before any such call report through debug mode and
+ * hidegs_queue_error only.
  */
 int hidegs_queue_error(void* stream, int clear, uint32_t* flags);
 

@@ -603,6 +603,50 @@ def test_async_failure_reported_on_its_own_stream_once_the_sort_has_run():
     assert var.hidegs_queue_error(ha, 1, C.byref(flags)) == 0 and flags.value == 0
 
 
+def test_async_failure_of_a_graph_replay_is_reported():
+    """A failing sort (the qcap build) captured into a hipGraph after an eager call has allocated the
+    asynchronous words (the slot must not be fixed to NULL in the graph).  The capture stream
+    is not the replay stream, so the captured sort reports to the graph word: after a replay the next call
+    on ANY stream returns HIDEGS_E_ASYNC once, naming the graph; the call after that runs."""
+    import ctypes as C
+
+    from hidegs_amd import _lib, build
+    var = _lib.load_library(build.variant_path("qcap"))
+    g = np.random.default_rng(17)
+    T = 1024
+    keys, _ = raster_like_keys(100_000, T, 7)
+    hot = (np.uint64(300) << np.uint64(32)) | g.uniform(0.5, 60.0, 200_000).astype(np.float32).view(
+        np.uint32).astype(np.uint64)
+    keys = np.concatenate([keys, hot])[g.permutation(300_000)]
+    kd, vd = u64(keys), u32(np.arange(keys.size, dtype=np.uint32))
+    x = torch.ones(1000, dtype=torch.int32, device="cuda")
+    tmp = torch.empty(var.hidegs_scan_scratch_bytes(1000), dtype=torch.uint8, device="cuda")
+    here = torch.cuda.current_stream().cuda_stream
+    # an eager call first: it allocates the words (a capture never does)
+    assert var.hidegs_inclusive_scan_u32(tmp.data_ptr(), tmp.numel(), x.data_ptr(), x.data_ptr(), 1000, here) == 0
+    ko, vo = torch.empty_like(kd), torch.empty_like(vd)
+    rng = torch.empty((T, 2), dtype=torch.int32, device="cuda")
+    scratch = torch.empty(int(var.hidegs_sort_pairs_u64_scratch_bytes(kd.numel())), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        rc = var.hidegs_sort_tile_pairs(_lib.ptr(scratch), scratch.numel(), _lib.ptr(kd), _lib.ptr(ko), _lib.ptr(vd),
+                                        _lib.ptr(vo), kd.numel(), T, _lib.ptr(rng),
+                                        torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    flags = C.c_uint32(0)
+    assert var.hidegs_queue_error(here, 1, C.byref(flags)) == 0  # capture ran nothing; clear the history
+    graph.replay()
+    torch.cuda.synchronize()
+    other = torch.cuda.Stream()
+    rc = var.hidegs_inclusive_scan_u32(tmp.data_ptr(), tmp.numel(), x.data_ptr(), x.data_ptr(), 1000, other.cuda_stream)
+    assert rc == _lib.E_ASYNC
+    assert b"replayed from a graph" in var.hidegs_last_error() and b"job slots exhausted" in var.hidegs_last_error()
+    assert var.hidegs_inclusive_scan_u32(tmp.data_ptr(), tmp.numel(), x.data_ptr(), x.data_ptr(), 1000, here) == 0
+    assert var.hidegs_queue_error(here, 1, C.byref(flags)) == 0 and flags.value & 1
+    torch.cuda.synchronize()
+
+
 def test_debug_mode_passes_clean_sorts():
     """Debug mode on the product build: synchronising checks and the queue check, no false alarm."""
     g = np.random.default_rng(12)
