@@ -225,10 +225,11 @@ def test_hot_tile_queue_beside_an_rccl_exchange_on_another_stream():
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("transport", ["fp32", "bf16"])
-def test_exchange_and_step_on_rccl_forced_single_rank(transport):
+@pytest.mark.parametrize("transport,blocking", [("fp32", False), ("bf16", False), ("fp32", True)])
+def test_exchange_and_step_on_rccl_forced_single_rank(transport, blocking):
     """The overlapped path on hardware (every bucket's collective issued, then per bucket its wait
-    and that bucket's rows' masked Adam step): equals Adam.step(visible) on the summed gradients."""
+    and that bucket's rows' masked Adam step): equals Adam.step(visible) on the summed gradients.
+    blocking=True: every RCCL wait bounded on the host (view_dp.py "Failure detection"), same result."""
     from hidegs_amd.optim import Adam
     from hidegs_amd.view_dp import LEAF_WIDTHS, GradArena, ViewDPExchange
     dist = _one_rank_nccl()
@@ -246,7 +247,8 @@ def test_exchange_and_step_on_rccl_forced_single_rank(transport):
             pa[k].grad = grads[k].to(torch.bfloat16).float() if transport == "bf16" else grads[k].clone()
             arena[k].copy_(grads[k])
         Adam(list(pa.values()), lr=0.01, eps=1e-15).step(visible)
-        ex = ViewDPExchange(bucket_bytes=256 << 10, compact_below=0.0, transport=transport, force_collectives=True)
+        ex = ViewDPExchange(bucket_bytes=256 << 10, compact_below=0.0, transport=transport, force_collectives=True,
+                            timeout=60, blocking=blocking)
         res = ex.exchange_and_step(arena, visible, Adam(list(pb.values()), lr=0.01, eps=1e-15), pb)
         torch.cuda.synchronize()
         assert ex.last.collectives > len(LEAF_WIDTHS) and torch.equal(res.union, visible)
