@@ -5,7 +5,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 python -c "import bench; print(bench.sources_sha256())" > gpurun_out/sources.sha256 && \
 date +%s.%N > gpurun_out/t_gputest0 && \
-HIDEGS_MAPS_OUT=gpurun_out/maps_gputest.txt timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider --durations=10 > gpurun_out/gputest.log 2>&1 && \
+HIDEGS_MAPS_OUT=gpurun_out/maps_gputest.txt timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider --durations=10 -s > gpurun_out/gputest.log 2>&1 && \
 date +%s.%N > gpurun_out/t_gputest1 && \
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
 date +%s.%N > gpurun_out/t_smoke1 && \

@@ -37,7 +37,7 @@ def main():
     sha = open(box_sha).read().strip() if os.path.exists(box_sha) else bench.sources_sha256()
     with open(os.path.join(P, "latest_kernels.meta.json"), "w") as f:
         json.dump({"commit": head[:12] + ("+uncommitted kernel edits" if dirty else ""), "sources_sha256": sha,
-                   "profile": name, "command": "tools/gpu_round5.sh: rocprofv3 --kernel-trace --stats, then "
+                   "profile": name, "command": "tools/gpu_round5.sh / gpu_round6.sh: rocprofv3 --kernel-trace --stats, then "
                    "--pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py", "note": note}, f, indent=1)
     shutil.copy(os.path.join(G, "prof_kt", "kt_kernel_stats.csv"), os.path.join(P, f"{name}_kernel_stats.csv"))
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_json.py"), os.path.join(G, "prof_knn"),
@@ -50,7 +50,7 @@ def main():
     tests = open(os.path.join(G, "gputest.log")).read().strip().splitlines()[-1]
     with open(os.path.join(P, f"{name}.md"), "w") as f:
         f.write(f"# {title}\n\n")
-        f.write(f"Command: `tools/gpu_round5.sh` ({note}; tests: {tests}; smoke; bench; rocprofv3 kernel trace; "
+        f.write(f"Command: `{os.environ.get('GPU_SCRIPT', 'tools/gpu_round5.sh')}` ({note}; tests: {tests}; smoke; bench; rocprofv3 kernel trace; "
                 "FETCH_SIZE / WRITE_SIZE passes; knn VALU pass).\n")
         f.write(f"Bench line: `{name}_bench.json`: binning step {b['ms_per_step']} ms (radix_scatter {r['avg_launch_us']} us "
                 f"in-bench = {r['frac']} of 8 TB/s; traffic {r['traffic'] / 1e6:.1f} MB against "
