@@ -199,7 +199,7 @@ def parse():
     ap.add_argument("--no-adam", action="store_true")
     ap.add_argument("--no-config5", action="store_true", help="skip the config 2 and config 5 scale sub-metrics")
     ap.add_argument("--no-skewed", action="store_true")
-    ap.add_argument("--pg-timeout", type=float, default=120.0,
+    ap.add_argument("--pg-timeout", type=float, default=300.0,
                     help="seconds: the process group's timeout (RCCL watchdog: a collective that never completes "
                          "ends the process) and the exchange's bounded host waits (gloo)")
     return ap.parse_args()
