@@ -30,7 +30,9 @@ def main():
     shutil.copy(kj, os.path.join(P, "latest_kernels.json"))
     sys.path.insert(0, ROOT)
     import bench
-    head = subprocess.run(["git", "rev-parse", "HEAD"], cwd=ROOT, capture_output=True, text=True).stdout.strip()
+    # PROFILE_COMMIT: the commit the session ran on, when HEAD has moved on since (tests or docs only)
+    head = os.environ.get("PROFILE_COMMIT") or subprocess.run(["git", "rev-parse", "HEAD"], cwd=ROOT,
+                                                              capture_output=True, text=True).stdout.strip()
     dirty = subprocess.run(["git", "status", "--porcelain", "hidegs_amd/csrc", "include"], cwd=ROOT,
                            capture_output=True, text=True).stdout.strip() != ""
     box_sha = os.path.join(G, "sources.sha256")  # written on the GPU box by the session script
