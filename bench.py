@@ -253,7 +253,8 @@ def main() -> None:
             os.environ["MASTER_PORT"] = str(free_port())
         kw = {"device_id": dev} if gpu else {}
         # fail fast: a rank that stalls or dies ends the run within the timeout instead of hanging
-        # it -- RCCL's watchdog aborts a collective older than this; gloo operations time out after it
+        # it -- the RCCL process group's watchdog ends a rank whose collective is older than this; gloo
+        # operations time out after it
         dist.init_process_group(args.backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=args.pg_timeout), **kw)
 
@@ -311,8 +312,8 @@ def main() -> None:
         "roofline": None,
         "cpu_baseline": None,
         "fail_fast": {"process_group_timeout_s": args.pg_timeout, "exchange_host_wait_timeout_s": args.pg_timeout,
-                      "rccl": "watchdog aborts a collective older than the process group timeout and ends the "
-                              "process; the exchange's waits are stream waits (no host block)",
+                      "rccl": "the watchdog ends a rank whose collective is older than the process group "
+                              "timeout; the exchange's waits are stream waits (no host block)",
                       "gloo": "every exchange wait bounded on the host, RuntimeError naming the collective"},
     }
     cam = synthetic.d2_camera(W_PX, H_PX)

@@ -61,8 +61,8 @@ on the ranks still waiting:
   abandoned operation, so a process exiting after the error takes up to that long to tear down.
 * device tensors (RCCL): a wait only makes the compute stream wait on the collective's stream --
   the host never blocks, which is what lets the bucket pipeline overlap.  A collective that never
-  completes is caught by the process group's watchdog after the process group's timeout, which aborts
-  the communicators and ends the process (TORCH_NCCL_ASYNC_ERROR_HANDLING, on by default): pass an
+  completes is caught by the process group's watchdog after the process group's timeout, which ends
+  the process (TORCH_NCCL_ASYNC_ERROR_HANDLING, on by default in torch 2.10): pass an
   explicit `timeout` to init_process_group (bench.py does).  `blocking=True` bounds the host wait by
   `timeout` on device tensors too and raises the same RuntimeError, at the price of a host wait per
   collective (the bucket overlap then depends on the host keeping ahead).
