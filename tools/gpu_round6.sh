@@ -4,7 +4,7 @@
 # hash (bench.sources_sha256); gpurun_out/maps_gputest.txt: the in-tree .so files the test process mapped.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 python -c "import bench; print(bench.sources_sha256())" > gpurun_out/sources.sha256 && \
-ls -l --time-style=+%s.%N hidegs_amd/libhidegs.so hidegs_amd/build/*.o hidegs_amd/csrc/* include/hidegs.h > gpurun_out/mtimes.txt && \
+ls -l --time-style=+%s.%N hidegs_amd/libhidegs.so hidegs_amd/csrc/* include/hidegs.h > gpurun_out/mtimes.txt && \
 date +%s.%N > gpurun_out/t_gputest0 && \
 HIDEGS_MAPS_OUT=gpurun_out/maps_gputest.txt timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider --durations=10 -s > gpurun_out/gputest.log 2>&1 && \
 date +%s.%N > gpurun_out/t_gputest1 && \
