@@ -366,8 +366,8 @@ EX_TIMEOUT, PG_TIMEOUT = 1.5, 5.0
 
 
 def worker_fail(rank, world, port, scenario, q):
-    """Rank 1 stops taking part at some point of the exchange (stall: sleeps; crash: exits 3); rank 0 must
-    raise RuntimeError naming the collective it waited on, within the exchange's timeout."""
+    """The last rank stops taking part at some point of the exchange (stall: sleeps; crash: exits 3); every
+    other rank must raise RuntimeError naming the collective it waited on, within the exchange's timeout."""
     import datetime
     import time
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -380,64 +380,69 @@ def worker_fail(rank, world, port, scenario, q):
         arena = GradArena(N)
         for k, v in grads.items():
             arena[k].copy_(v)
-        if rank == 1:
+        if rank == world - 1:
             if scenario != "stall_visibility":
                 union, _ = ex.gather_visibility(visible)
             if scenario == "stall_max":
                 ex.sum_gradients(arena, union)
             if scenario == "crash_buckets":
                 os._exit(3)
-            time.sleep(600)  # stalled: the launcher (here the test) ends it once rank 0 has failed
+            time.sleep(600)  # stalled: the launcher (here the test) ends it once the others have failed
             return
         t0 = time.perf_counter()
         try:
             ex.exchange(arena, visible, max_stats=[norm])
         except RuntimeError as e:
-            q.put((str(e), time.perf_counter() - t0))
+            q.put((rank, str(e), time.perf_counter() - t0))
             raise
-        q.put(("no error", time.perf_counter() - t0))
+        q.put((rank, "no error", time.perf_counter() - t0))
     finally:
-        if rank == 0:
+        if rank != world - 1:
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("scenario,what", [
-    ("stall_visibility", "visibility all-gather"),
-    ("stall_buckets", "gradient bucket 1 of "),
-    ("stall_bf16", "bf16 all-to-all"),
-    ("stall_max", "MAX all-reduce"),
-    ("crash_buckets", "gradient bucket 1 of "),
+@pytest.mark.parametrize("world,scenario,what", [
+    (2, "stall_visibility", "visibility all-gather"),
+    (2, "stall_buckets", "gradient bucket 1 of "),
+    (2, "stall_bf16", "bf16 all-to-all"),
+    (2, "stall_max", "MAX all-reduce"),
+    (2, "crash_buckets", "gradient bucket 1 of "),
+    (8, "stall_buckets", "gradient bucket "),  # the driver's scaling width: seven ranks wait on the eighth
 ])
-def test_a_rank_that_stops_participating_fails_the_others_fast(scenario, what):
-    """SURVEY §5 "DP: fail fast" (VERDICT r05 item 2): gloo world 2, rank 1 stalls or dies mid-exchange.
-    Rank 0 raises RuntimeError naming the collective within the exchange timeout plus a small margin, and
-    every child exits non-zero instead of hanging (rank 0 after at most the process group's timeout;
-    the stalled rank is ended by its launcher, as torch.distributed.run ends the others when one fails)."""
+def test_a_rank_that_stops_participating_fails_the_others_fast(world, scenario, what):
+    """SURVEY §5 "DP: fail fast" (VERDICT r05 item 2): gloo, the last rank stalls or dies mid-exchange.
+    Every other rank raises RuntimeError naming the collective within the exchange timeout plus a small
+    margin, and every child exits non-zero instead of hanging (the waiting ranks after at most the process
+    group's timeout; the stalled rank is ended by its launcher, as torch.distributed.run ends the others
+    when one fails)."""
     import time
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker_fail, args=(r, 2, port, scenario, q)) for r in range(2)]
+    procs = [ctx.Process(target=worker_fail, args=(r, world, port, scenario, q)) for r in range(world)]
     for p in procs:
         p.start()
     try:
-        msg, elapsed = q.get(timeout=60)
+        got = [q.get(timeout=60) for _ in range(world - 1)]
         t_err = time.perf_counter()
-        procs[0].join(PG_TIMEOUT + 30)
+        for p in procs[:-1]:
+            p.join(PG_TIMEOUT + 30)
         exit_after = time.perf_counter() - t_err
     finally:
         for p in procs:
             if p.is_alive():
                 p.terminate()
             p.join(10)
-    print(f"{scenario}: raised after {elapsed:.2f} s, exited {exit_after:.1f} s later: {msg[:200]}")
-    assert what in msg and "did not complete" in msg and "rank 0 of 2" in msg, msg
-    if scenario.startswith("stall"):
-        assert f"waited at most {EX_TIMEOUT:g} s" in msg and "timed out" in msg, msg
-    assert elapsed < EX_TIMEOUT + 3.0, f"raised after {elapsed:.1f} s"
-    assert procs[0].exitcode not in (0, None), procs[0].exitcode
-    assert exit_after < PG_TIMEOUT + 15, f"rank 0 took {exit_after:.1f} s to exit after the error"
-    assert procs[1].exitcode not in (0, None), procs[1].exitcode
+    assert sorted(r for r, _, _ in got) == list(range(world - 1))
+    for rank, msg, elapsed in got:
+        print(f"{scenario} world {world} rank {rank}: raised after {elapsed:.2f} s: {msg[:160]}")
+        assert what in msg and "did not complete" in msg and f"rank {rank} of {world}" in msg, msg
+        if scenario.startswith("stall"):
+            assert f"waited at most {EX_TIMEOUT:g} s" in msg and "timed out" in msg, msg
+        assert elapsed < EX_TIMEOUT + 3.0, f"rank {rank} raised after {elapsed:.1f} s"
+    print(f"{scenario} world {world}: the waiting ranks exited {exit_after:.1f} s after the errors")
+    assert all(p.exitcode not in (0, None) for p in procs), [p.exitcode for p in procs]
+    assert exit_after < PG_TIMEOUT + 15, f"the waiting ranks took {exit_after:.1f} s to exit after the error"
 
 
 def test_timeout_is_checked():
