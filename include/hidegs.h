@@ -194,7 +194,7 @@ int hidegs_sort_tile_pairs(void* scratch, size_t scratch_bytes, const uint64_t* 
  * exhausted, bit 4 = a queue worker gave up waiting.  Non-zero means some sort since the last
  * clear returned pairs that are not fully sorted.  Synchronises `stream`; clear != 0 resets it (one
  * device-side exchange, so no error raised meanwhile is lost) and also takes `stream`'s asynchronous
- * word below.
+ * word and the graph word below.
  * Asynchronous report (no host synchronisation per sort): outside debug mode a failing sort's last
  * kernel ORs the failure into a word of mapped host memory that belongs to the sort's stream.  A later
  * compute entry-point call on that stream, made once that kernel has run, finds the word set, takes it
