@@ -1,7 +1,7 @@
 """Write profiles/<NAME>.md, <NAME>_bench.json, <NAME>_kernels.json, <NAME>_kernel_stats.csv and refresh
 profiles/latest_kernels.json / latest_knn_pmc.json (+ latest_kernels.meta.json: the commit and the kernel
 sources' hash the profile was taken on, which bench.py reports beside the traffic it reads) from a
-tools/gpu_round5.sh run in gpurun_out/.
+tools/gpu_round6.sh run (or $GPU_SCRIPT) in gpurun_out/.
 
 usage: python tools/profile_note.py NAME "title" "command / commit note"
 """
@@ -52,7 +52,7 @@ def main():
     tests = open(os.path.join(G, "gputest.log")).read().strip().splitlines()[-1]
     with open(os.path.join(P, f"{name}.md"), "w") as f:
         f.write(f"# {title}\n\n")
-        f.write(f"Command: `{os.environ.get('GPU_SCRIPT', 'tools/gpu_round5.sh')}` ({note}; tests: {tests}; smoke; bench; rocprofv3 kernel trace; "
+        f.write(f"Command: `{os.environ.get('GPU_SCRIPT', 'tools/gpu_round6.sh')}` ({note}; tests: {tests}; smoke; bench; rocprofv3 kernel trace; "
                 "FETCH_SIZE / WRITE_SIZE passes; knn VALU pass).\n")
         f.write(f"Bench line: `{name}_bench.json`: binning step {b['ms_per_step']} ms (radix_scatter {r['avg_launch_us']} us "
                 f"in-bench = {r['frac']} of 8 TB/s; traffic {r['traffic'] / 1e6:.1f} MB against "
