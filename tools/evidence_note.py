@@ -7,6 +7,7 @@ the tests printed about when asynchronous errors surfaced.
 usage: python tools/evidence_note.py NAME
 """
 import os
+import re
 import subprocess
 import sys
 
@@ -31,7 +32,8 @@ def main():
     t0, t1, t2 = (float(read(n)) for n in ("t_gputest0", "t_gputest1", "t_smoke1"))
     log = read("gputest.log").splitlines()
     summary = log[-1]
-    printed = [ln for ln in log if ln.startswith(("HIDEGS_E_ASYNC", "stall_", "crash_"))]
+    # pytest -q -s prints its progress dots on the same line as the test's own output
+    printed = [m.group(0) for ln in log for m in [re.search(r"(HIDEGS_E_ASYNC|stall_|crash_).*", ln)] if m]
     slow = []
     in_dur = False
     for ln in log:
