@@ -4,7 +4,8 @@ the commit, the kernel sources' hash, the `pytest -m gpu` pass line and wall tim
 the in-tree .so files the test process mapped, the command that builds every one of them, and the lines
 the tests printed about when asynchronous errors surfaced.
 
-usage: python tools/evidence_note.py NAME
+usage: python tools/evidence_note.py NAME [COMMIT]   (COMMIT: the commit the gpurun snapshot was taken at;
+       default HEAD -- give it when tools/ or profiles/ commits landed after the run)
 """
 import os
 import re
@@ -26,9 +27,11 @@ def main():
     missing = [n for n in need if not os.path.exists(os.path.join(G, n))]
     if missing:  # a failed or partial session: write nothing
         sys.exit(f"evidence_note: missing {missing}")
-    head = subprocess.run(["git", "rev-parse", "HEAD"], cwd=ROOT, capture_output=True, text=True).stdout.strip()
-    dirty = subprocess.run(["git", "status", "--porcelain", "--", ".", ":!profiles", ":!gpurun_out"], cwd=ROOT,
-                           capture_output=True, text=True).stdout.strip()
+    rev = sys.argv[2] if len(sys.argv) > 2 else "HEAD"
+    head = subprocess.run(["git", "rev-parse", rev], cwd=ROOT, capture_output=True, text=True).stdout.strip()
+    dirty = "" if rev != "HEAD" else subprocess.run(
+        ["git", "status", "--porcelain", "--", ".", ":!profiles", ":!gpurun_out"], cwd=ROOT, capture_output=True,
+        text=True).stdout.strip()
     t0, t1, t2 = (float(read(n)) for n in ("t_gputest0", "t_gputest1", "t_smoke1"))
     log = read("gputest.log").splitlines()
     summary = log[-1]
